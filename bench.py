@@ -1,0 +1,293 @@
+"""Benchmark: Flow.log_prob samples/s (+ NLL) on the BASELINE.json headline
+config — 4D rolling spline coupling flow, K=16 knots, 4 couplings, hidden
+(128, 128), Normal latent, batch 2^20 per GPU — through the fused HIP kernel.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+
+One process per GPU (torch.distributed.run for N>1; torch is only the control
+plane: barrier, max-over-ranks timing, RCCL unique-id broadcast).  A step is
+one log_prob pass over the resident 2^20-row shard: the fused kernel
+(ShiftBounds -> 4x[MLP on fp32 MFMA + RQ spline] -> Normal latent -> NaN->-inf
+-> per-block NLL partials), the fp64 NLL reduce and, for N>1, the RCCL
+all-reduce of the NLL.  Rank 0 prints one JSON line."""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (no xf32 on gfx950)
+PEAK_HBM_GBS = 8000.0
+
+WORKLOADS = {
+    # name: (D, C, K, layers, couplings, latent, mode)
+    "cfg2": (4, 0, 16, (128, 128), 4, "normal", "log_prob"),
+    "cfg3": (4, 0, 16, (128, 128), 4, "normal", "inverse"),
+    "cfg4": (2, 2, 16, (128, 128), 2, "beta", "log_prob"),
+    "cfg5": (16, 0, 32, (256, 256), 8, "normal", "log_prob"),
+}
+
+
+def build_model(name):
+    import zenflow_amd as zf
+    from zenflow_amd import bijectors as bi
+    from zenflow_amd import distributions as dist
+
+    D, C, K, layers, L, latent, mode = WORKLOADS[name]
+    bij = [bi.ShiftBounds(margin=0.1)]
+    for _ in range(L - 1):
+        bij += [bi.NeuralSplineCoupling(knots=K, layers=layers), bi.Roll()]
+    bij.append(bi.NeuralSplineCoupling(knots=K, layers=layers))
+    lat = dist.Normal() if latent == "normal" else dist.Beta()
+    return zf.Flow(bi.Chain(bij), latent=lat)
+
+
+def flops_per_sample(name):
+    """2 * MACs of the conditioner MLPs: 2*L*[(dc+C)H + H*H + H*dt*S]."""
+    D, C, K, layers, L, _, _ = WORKLOADS[name]
+    dt, dc = D // 2, D - D // 2
+    widths = [dc + C] + list(layers) + [dt * (3 * K - 1)]
+    return 2 * L * sum(a * b for a, b in zip(widths[:-1], widths[1:]))
+
+
+def cpu_baseline(model_spec, variables, x, c, budget_s=10.0):
+    """The oracle (NumPy fp32 restatement of the reference graph) on the host
+    cores, on a bounded sample of the same workload."""
+    from oracle import zf_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    chunk = 1 << 13
+    done, t0, outs = 0, time.perf_counter(), []
+    while True:
+        lo = done % x.shape[0]
+        xs = x[lo : lo + chunk]
+        cs = None if c is None else c[lo : lo + chunk]
+        lp, _ = O.flow_log_prob(model_spec, variables, xs, cs)
+        outs.append((lo, lp))
+        done += xs.shape[0]
+        el = time.perf_counter() - t0
+        if el >= budget_s or done >= x.shape[0]:
+            break
+    return {
+        "value": done / el,
+        "unit": "samples/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": f"{done} rows of the same 2^20-row batch in {chunk}-row chunks, {el:.1f} s, "
+                  f"NumPy fp32 oracle (JAX-CPU reference not importable); BLAS threads={threads}",
+        "host_cpus": len(os.sched_getaffinity(0)),
+    }, outs
+
+
+def oracle_spec(name):
+    D, C, K, layers, L, latent, _ = WORKLOADS[name]
+    bij = [{"type": "shift_bounds", "margin": 0.1, "bounds": ()}]
+    for _ in range(L - 1):
+        bij += [{"type": "nsc", "knots": K, "layers": list(layers)}, {"type": "roll", "shift": 1}]
+    bij.append({"type": "nsc", "knots": K, "layers": list(layers)})
+    return {"bijector": {"type": "chain", "bijectors": bij}, "latent": {"type": latent}}
+
+
+def load_traffic(kernel_prefix, launches_per_step):
+    """HBM bytes per launch from the committed PMC summary (profiles/), or None."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--rows-log2", type=int, default=20, help="rows per GPU = 2^k")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    td = None
+    if world > 1:
+        import torch.distributed as td
+
+        td.init_process_group("gloo")
+
+    def barrier():
+        if td is not None:
+            td.barrier()
+
+    import zenflow_amd as zf
+    from zenflow_amd import _lib as L
+    from zenflow_amd._lib import DeviceArray, Event
+    from zenflow_amd.dist import RcclCommunicator
+    from zenflow_amd.random import PRNGKey
+
+    L.ensure_device()
+    name = args.config
+    D, C, K, layers, nL, latent, mode = WORKLOADS[name]
+    N = 1 << args.rows_log2
+    flow = build_model(name)
+    # Random-init weights of the named architecture (flax default initialisers),
+    # then one train-mode pass over a separate 2^16 batch to set the ShiftBounds
+    # min/max and BatchNorm running statistics.
+    xinit = np.random.default_rng(3).standard_normal((1 << 16, D)).astype(np.float32)
+    cinit = np.random.default_rng(4).standard_normal((1 << 16, C)).astype(np.float32) if C else None
+    variables = flow.init(PRNGKey(1), xinit[:1], None if cinit is None else cinit[:1])
+    _, upd = flow.apply(variables, xinit, cinit, train=True, mutable=["batch_stats"])
+    variables = {"params": variables["params"], "batch_stats": upd["batch_stats"]}
+
+    rng = np.random.default_rng(1000 + rank)
+    x = rng.standard_normal((N, D)).astype(np.float32)  # synthetic Gaussian shard
+    if mode == "inverse":
+        x = (0.5 + 0.1 * rng.standard_normal((N, D))).astype(np.float32)
+    c = rng.standard_normal((N, C)).astype(np.float32) if C else None
+    bf = flow.bind(variables, D, C)
+    prog = bf.program
+    xd = DeviceArray.from_numpy(x)
+    cd = DeviceArray.from_numpy(c) if C else None
+    out = DeviceArray((N,)) if mode == "log_prob" else DeviceArray((N, D))
+    nll = DeviceArray((1,), np.float64)
+    ws = prog.workspace(N)
+    lib = L.load_library()
+    comm = None
+    if world > 1:
+        def bcast(b):
+            obj = [b]
+            td.broadcast_object_list(obj, src=0)
+            return obj[0]
+
+        comm = RcclCommunicator(rank, world, bcast)
+
+    n_ops = len(prog.ops)
+    events = []
+
+    def step(ev=None):
+        if mode == "log_prob":
+            if ev is not None:
+                ev[0].record()
+            L.check(lib.zf_flow_log_prob_segment(prog.handle, 0, n_ops, xd.ptr, None if cd is None else cd.ptr,
+                                                 None, out.ptr, None, ws.ptr, N, L.stream()), "log_prob")
+            if ev is not None:
+                ev[1].record()
+            L.check(lib.zf_flow_nll_reduce(ws.ptr, N, nll.ptr, L.stream()), "nll_reduce")
+            if comm is not None:
+                comm.allreduce_sum_(nll)
+        else:
+            if ev is not None:
+                ev[0].record()
+            prog.inverse(xd, cd, out=out)
+            if ev is not None:
+                ev[1].record()
+
+    for _ in range(args.warmup):
+        step()
+    L.synchronize()
+    evs = [(Event(), Event()) for _ in range(args.steps)]
+    barrier()
+    L.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    L.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if td is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_ms(b) for (a, b) in evs]
+    kavg = float(np.mean(kern_ms))
+    ms_per_step = 1e3 * elapsed / args.steps
+    total = N * world * args.steps
+    value = total / elapsed
+
+    fps = flops_per_sample(name)
+    achieved = fps * N / (kavg * 1e-3) / 1e12
+    kernel_name = "flow_kernel"
+    traffic = load_traffic(kernel_name, 1)
+    result = {
+        "metric": "log_prob samples/sec (+ NLL match) 4D 16-knot 4-layer flow, batch 2^20"
+        if name == "cfg2" else f"{mode} samples/sec ({name})",
+        "value": value,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: x ~ N(0, I) per rank; random-init weights (flax default initialisers) "
+                "+ one train-mode pass for ShiftBounds/BatchNorm statistics",
+        "config": {
+            "workload": f"{name}: Flow(rolling_spline_coupling({D}, knots={K}, layers={list(layers)})"
+                        f"{' x' + str(nL) + ' couplings' if nL != D else ''}, latent={latent}).{mode}, "
+                        f"{N} rows per GPU, resident in HBM",
+            "rows_per_gpu": N,
+            "global_batch": N * world,
+            "parallelism": f"dp{world} (batch shards, RCCL all-reduce of the fp64 NLL)",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+            "traffic": traffic,
+            "kernel": f"{kernel_name} (avg {kavg * 1e3:.1f} us over {args.steps} timed launches, HIP events)",
+            "alg_flops_per_sample": fps,
+        },
+    }
+    if mode == "log_prob":
+        result["nll"] = -float(nll.numpy()[0]) / (N * world)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        spec = oracle_spec(name)
+        if mode == "log_prob":
+            cb, outs = cpu_baseline(spec, variables, x, c, args.cpu_budget)
+            lp = out.numpy()
+            errs, mism = [], 0
+            for lo, ref in outs:
+                g = lp[lo : lo + ref.shape[0]]
+                f = np.isfinite(ref) & np.isfinite(g)
+                mism += int((np.isfinite(ref) != np.isfinite(g)).sum())
+                errs.append(float((np.abs(g[f] - ref[f]) / np.maximum(1, np.abs(ref[f]))).max()))
+            result["parity"] = {"rows_checked": int(sum(o[1].shape[0] for o in outs)),
+                                "max_rel_err_vs_oracle": max(errs), "finiteness_mismatches": mism,
+                                "tolerance": 1e-5}
+            result["cpu_baseline"] = cb
+            result["speedup_vs_cpu"] = value / cb["value"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.close()
+    if td is not None:
+        td.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,234 @@
+/*
+ * zenflow_amd.h — C ABI of the MI355X-native zenflow hot path (libzenflow_amd.so).
+ *
+ * The reference (HDembinski/zenflow, a JAX/FLAX library) has no FFI: its
+ * boundary is the FLAX module protocol.  Each entry point below replaces one
+ * reference callable (cited file:line, relative to the reference repo); the
+ * Python package `zenflow_amd` binds them with ctypes and re-exposes the
+ * reference's names and signatures (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Device pointers come from zf_malloc (or
+ *     any hipMalloc'ed buffer); `stream` is a hipStream_t passed as void*
+ *     (NULL = the legacy default stream).
+ *   - Every function returns 0 on success, a negative ZF_E* code on a bad
+ *     argument, or a positive hipError_t.  zf_last_error() returns a
+ *     thread-local message for the last failure.
+ *   - All floating-point data is fp32, row-major; log-det / NLL partial sums
+ *     are fp64.  Kernels never trap on NaN/Inf: they propagate exactly as the
+ *     reference does.
+ */
+#ifndef ZENFLOW_AMD_H
+#define ZENFLOW_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZF_OK 0
+#define ZF_EINVAL (-1)     /* invalid argument / shape */
+#define ZF_ENOTSUP (-2)    /* configuration not supported by the kernels */
+#define ZF_ENOMEM (-3)
+
+/* ------------------------------------------------------------------------ */
+/* Runtime: devices, memory, streams, events (plumbing for the host layer).  */
+/* ------------------------------------------------------------------------ */
+const char* zf_last_error(void);
+int zf_version(void);
+int zf_device_count(int* count);
+int zf_set_device(int device);
+int zf_get_device(int* device);
+int zf_device_name(int device, char* buf, int buflen);
+int zf_device_synchronize(void);
+int zf_malloc(void** ptr, size_t bytes);
+int zf_free(void* ptr);
+int zf_memset_async(void* ptr, int value, size_t bytes, void* stream);
+int zf_memcpy_htod(void* dst, const void* src, size_t bytes, void* stream);
+int zf_memcpy_dtoh(void* dst, const void* src, size_t bytes, void* stream);
+int zf_memcpy_dtod(void* dst, const void* src, size_t bytes, void* stream);
+int zf_stream_create(void** stream);
+int zf_stream_destroy(void* stream);
+int zf_stream_synchronize(void* stream);
+int zf_event_create(void** event);
+int zf_event_destroy(void* event);
+int zf_event_record(void* event, void* stream);
+int zf_event_elapsed_ms(void* start, void* stop, float* ms);
+int zf_event_synchronize(void* event);
+
+/* ------------------------------------------------------------------------ */
+/* K1 — spline numerics at the `zenflow.utils` boundary.                     */
+/* ------------------------------------------------------------------------ */
+/* Replaces utils.rational_quadratic_spline_forward (src/zenflow/utils.py:65-141).
+ * x (M,N), dx/dy (M,N,K) normalised widths/heights, slope (M,N,K-1) inner knot
+ * derivatives -> y (M,N), log_det (M,) = sum over N of log dy/dx.
+ * y and/or log_det may be NULL. */
+int zf_rqs_forward(const float* x, const float* dx, const float* dy, const float* slope,
+                   float* y, float* log_det, int64_t M, int N, int K, void* stream);
+
+/* Replaces utils.rational_quadratic_spline_inverse (src/zenflow/utils.py:144-202). */
+int zf_rqs_inverse(const float* y, const float* dx, const float* dy, const float* slope,
+                   float* x, int64_t M, int N, int K, void* stream);
+
+/* Replaces utils.squareplus (src/zenflow/utils.py:18-20), elementwise, b = 4 by default. */
+int zf_squareplus(const float* x, float* y, int64_t n, float b, void* stream);
+
+/* Replaces utils.softmax_with_threshold (src/zenflow/utils.py:23-34) over rows of K. */
+int zf_softmax_with_threshold(const float* x, float* y, int64_t M, int K, double threshold,
+                              void* stream);
+
+/* Replaces utils.normalize_spline_params (src/zenflow/utils.py:37-62):
+ * raw (M, K) / (M, K) / (M, K-1) logits -> normalised, written in place. */
+int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, int K,
+                               void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Fused flow program: ShiftBounds / NeuralSplineCoupling / Roll / latent.   */
+/* ------------------------------------------------------------------------ */
+
+/* Op kinds of a flow program (one per reference bijector). */
+#define ZF_OP_SHIFT_BOUNDS 1 /* bijectors.ShiftBounds         bijectors.py:132-273 */
+#define ZF_OP_ROLL 2         /* bijectors.Roll                bijectors.py:276-297 */
+#define ZF_OP_NSC 3          /* bijectors.NeuralSplineCoupling bijectors.py:300-371 */
+
+/* Latent log_prob epilogues (distributions.py). */
+#define ZF_LATENT_NONE 0
+#define ZF_LATENT_NORMAL 1    /* distributions.py:50-62  */
+#define ZF_LATENT_BETA 2      /* distributions.py:81-116 */
+#define ZF_LATENT_TRUNCNORM 3 /* distributions.py:65-78  */
+#define ZF_LATENT_UNIFORM 4   /* distributions.py:119-126 */
+
+/* Activation of the conditioner's hidden layers (NSC.act, bijectors.py:319). */
+#define ZF_ACT_SWISH 0
+
+/* ShiftBounds per-dim modes (bijectors.py:183-205). */
+#define ZF_SB_NONE 0  /* unbounded: running min/max affine + clip        */
+#define ZF_SB_BOTH 1  /* (a, b) both finite: fixed affine                */
+#define ZF_SB_LOWER 2 /* only a: t = safe_log(x - a), then min/max affine */
+#define ZF_SB_UPPER 3 /* only b: t = safe_log(b - x), then min/max affine */
+
+typedef struct zf_op_desc {
+  int32_t kind;       /* ZF_OP_* */
+  /* ROLL */
+  int32_t shift;      /* jnp.roll shift along the last axis */
+  /* NSC */
+  int32_t knots;      /* K (2 <= K <= 64) */
+  int32_t n_hidden;   /* number of hidden Dense layers (len(layers)), 1..16 */
+  int32_t hidden[16]; /* widths of the hidden layers (each <= 256) */
+  int32_t act;        /* ZF_ACT_* */
+  int32_t _pad;
+  /* Offsets (in floats) into the NATURAL parameter blob, filled by
+   * zf_flow_plan.  The natural blob holds exactly the FLAX variables:
+   *   NSC:  off_bn -> BatchNorm_0 {mean[DC], var[DC], scale[DC], bias[DC]}
+   *         (DC = D - D/2 + C conditioner inputs),
+   *         off_w[l] -> Dense_l.kernel, row-major (in_l, out_l),
+   *         off_b[l] -> Dense_l.bias (out_l); l = 0..n_hidden, the last layer
+   *         has out = (D/2)*(3K-1) (bijectors.py:343-347).
+   *   SHIFT_BOUNDS: off_sb -> per dim 8 floats {mode(ZF_SB_*), a, b, xmin, xmax, 0, 0, 0}
+   *         (batch_stats xmin_i / xmax_i, bijectors.py:243-248). */
+  int64_t off_bn;
+  int64_t off_w[17];
+  int64_t off_b[17];
+  int64_t off_sb;
+} zf_op_desc;
+
+typedef struct zf_flow_desc {
+  int32_t dim;        /* D: data dims (2..64 when the flow has an NSC) */
+  int32_t cond_dim;   /* C: condition dims (0 = unconditional) */
+  int32_t latent;     /* ZF_LATENT_* */
+  float latent_param; /* Beta peakness */
+  int32_t n_ops;      /* <= 64 */
+  int32_t _pad;
+  zf_op_desc ops[64];
+} zf_flow_desc;
+
+typedef struct zf_flow zf_flow_t; /* opaque handle: device-resident packed weights */
+
+/* Validate `desc` and fill its natural-blob offsets; *blob_floats = size of
+ * the natural blob.  Host-side only. */
+int zf_flow_plan(zf_flow_desc* desc, int64_t* blob_floats);
+
+/* Pack the natural blob into the device layout (MFMA fragment order, BN
+ * folded to (mean, rsqrt(var+eps)*scale, bias), ShiftBounds mul/log(mul))
+ * and copy it to the current device.  The handle owns the device copy until
+ * zf_flow_destroy. */
+int zf_flow_create(const zf_flow_desc* desc, const float* blob_host, int64_t blob_floats,
+                   zf_flow_t** handle);
+int zf_flow_destroy(zf_flow_t* handle);
+
+/* Device workspace needed by zf_flow_log_prob for N rows. */
+int64_t zf_flow_workspace_bytes(int64_t N);
+
+/* Replaces Flow.__call__ = log_prob (src/zenflow/flow.py:22-48), eval mode:
+ * x (N,D), c (N,C) or NULL -> log_prob (N,) with NaN -> -inf, +-inf -> +-FLT_MAX
+ * (jnp.nan_to_num, flow.py:47).  If nll_sum != NULL, the per-block fp64
+ * partial sums of log_prob are reduced on device into nll_sum[0]
+ * (NLL = -nll_sum/N, train.py:75-78). */
+int zf_flow_log_prob(zf_flow_t* h, const float* x, const float* c, float* log_prob,
+                     double* nll_sum, void* workspace, int64_t N, void* stream);
+
+/* Segment form of zf_flow_log_prob: runs ops [op_begin, op_end) on x, seeds
+ * the log-det accumulator from log_det_in (may be NULL), then applies the
+ * latent epilogue (train mode runs the bijectors segment by segment).  With a
+ * workspace the kernel writes per-block fp64 partial sums of log_prob there;
+ * with nll_sum it also reduces them (else call zf_flow_nll_reduce). */
+int zf_flow_log_prob_segment(zf_flow_t* h, int op_begin, int op_end, const float* x,
+                             const float* c, const float* log_det_in, float* log_prob,
+                             double* nll_sum, void* workspace, int64_t N, void* stream);
+
+/* Fixed-order fp64 sum of the per-block partials a log_prob launch left in
+ * `workspace` for N rows -> nll_sum[0] (= sum log_prob; NLL = -nll_sum/N). */
+int zf_flow_nll_reduce(const void* workspace, int64_t N, double* nll_sum, void* stream);
+
+/* Replaces Chain.__call__ (bijectors.py:103-111) over the op range
+ * [op_begin, op_end): x (N,D) -> y (N,D), log_det (N,).  If log_det_in is not
+ * NULL its values seed the accumulator (chained segments, train mode). */
+int zf_flow_forward(zf_flow_t* h, int op_begin, int op_end, const float* x, const float* c,
+                    float* y, const float* log_det_in, float* log_det, int64_t N,
+                    void* stream);
+
+/* Replaces Chain.inverse (bijectors.py:113-116) / the bijector half of
+ * Flow.sample (flow.py:70-78) over [op_begin, op_end), applied in reverse:
+ * z (N,D) -> x (N,D). */
+int zf_flow_inverse(zf_flow_t* h, int op_begin, int op_end, const float* z, const float* c,
+                    float* x, int64_t N, void* stream);
+
+/* Replace one NSC op's BatchNorm statistics (mean[DC], var[DC]) — flax
+ * BatchNorm with use_running_average=False normalises by batch statistics. */
+int zf_flow_set_bn_stats(zf_flow_t* h, int op, const float* mean, const float* var);
+
+/* Replace one ShiftBounds op's per-dim xmin/xmax (bijectors.py:250-263). */
+int zf_flow_set_sb_stats(zf_flow_t* h, int op, const float* xmin, const float* xmax);
+
+/* ------------------------------------------------------------------------ */
+/* Train-mode batch statistics (reductions over the batch axis).             */
+/* ------------------------------------------------------------------------ */
+/* Per column j (0 <= j < ncols) of x (N rows, row stride `ld` floats, first
+ * column `col_offset`): min, max (fp32, NaN-propagating like jnp.min/max) and
+ * sum, sum of squares (fp64).  ShiftBounds' batch min/max (bijectors.py:250-257)
+ * and flax BatchNorm's batch mean/var (bijectors.py:342, train=True).
+ * pre_modes/pre_params (host arrays of ncols, or NULL): per column ZF_SB_LOWER
+ * -> safe_log(x - a), ZF_SB_UPPER -> safe_log(a - x) with a = pre_params[j]
+ * (the one-sided-bound transform, bijectors.py:193-202).  Outputs are device
+ * pointers (any may be NULL); workspace: zf_colstats_workspace_bytes(N, ncols). */
+int64_t zf_colstats_workspace_bytes(int64_t N, int ncols);
+int zf_colstats(const float* x, int64_t N, int ncols, int64_t ld, int col_offset,
+                const float* pre_modes, const float* pre_params, float* cmin, float* cmax,
+                double* csum, double* csumsq, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* RCCL (over xGMI) — all-reduce of the fp64 NLL partial across ranks.       */
+/* ------------------------------------------------------------------------ */
+int zf_rccl_available(void);
+int zf_rccl_get_unique_id(char* id128);
+int zf_rccl_comm_init(void** comm, int nranks, const char* id128, int rank);
+int zf_rccl_allreduce_sum_f64(void* comm, const double* send, double* recv, size_t count,
+                              void* stream);
+int zf_rccl_comm_destroy(void* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZENFLOW_AMD_H */

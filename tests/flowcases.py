@@ -1,0 +1,114 @@
+"""Shared test cases: flow configurations (BASELINE.json configs), FLAX-layout
+variables and synthetic inputs, built without touching the product code.
+
+``make_case`` returns the oracle model spec, the variables pytree (exactly the
+tree FLAX would hold for ``Flow(rolling_spline_coupling(D, ...))``) and
+seeded inputs.  The GPU tests build the matching zenflow_amd module with
+``build_flow`` and feed it the same variables."""
+
+from __future__ import annotations
+
+import numpy as np
+
+# BASELINE.json configs; N here is the test size.
+CONFIGS = {
+    "cfg1": dict(D=2, C=0, K=8, layers=(128, 128), latent="beta"),  # two_moons
+    "cfg2": dict(D=4, C=0, K=16, layers=(128, 128), latent="normal"),  # 4D fwd / inv
+    "cfg4": dict(D=2, C=2, K=16, layers=(128, 128), latent="beta"),  # two_moons_conditional
+    "cfg4c1": dict(D=2, C=1, K=16, layers=(128, 128), latent="beta"),  # ref NB: 1-D label
+    "cfg5": dict(D=16, C=0, K=32, layers=(256, 256), latent="normal", couplings=8),
+    "small": dict(D=3, C=0, K=5, layers=(64, 64), latent="normal"),
+    "odd": dict(D=5, C=3, K=7, layers=(48, 96, 32), latent="truncated_normal"),
+    "uniform": dict(D=2, C=0, K=4, layers=(32,), latent="uniform"),
+    "deep": dict(D=2, C=8, K=16, layers=(128,) * 6, latent="beta"),  # deep_set NB shape
+}
+
+
+def chain_spec(cfg):
+    D, K, layers = cfg["D"], cfg["K"], list(cfg["layers"])
+    L = cfg.get("couplings", D)
+    bij = [{"type": "shift_bounds", "margin": cfg.get("margin", 0.1), "bounds": cfg.get("bounds", ())}]
+    for _ in range(L - 1):
+        bij.append({"type": "nsc", "knots": K, "layers": layers})
+        bij.append({"type": "roll", "shift": 1})
+    bij.append({"type": "nsc", "knots": K, "layers": layers})
+    return {"type": "chain", "bijectors": bij}
+
+
+def _lecun(rng, fan_in, fan_out):
+    std = np.sqrt(1.0 / fan_in) / 0.87962566103423978
+    z = np.clip(rng.standard_normal((fan_in, fan_out)), -2, 2)
+    return (z * std).astype(np.float32)
+
+
+def make_variables(cfg, rng, bias_scale=0.3):
+    D, C, K = cfg["D"], cfg["C"], cfg["K"]
+    spec = chain_spec(cfg)
+    dt = D // 2
+    DC = D - dt + C
+    params, stats = {}, {}
+    for i, b in enumerate(spec["bijectors"]):
+        key = f"bijectors_{i}"
+        if b["type"] == "nsc":
+            p = {
+                "BatchNorm_0": {
+                    "scale": (1 + 0.1 * rng.standard_normal(DC)).astype(np.float32),
+                    "bias": (0.1 * rng.standard_normal(DC)).astype(np.float32),
+                }
+            }
+            fan_in = DC
+            for l, w in enumerate(list(b["layers"]) + [dt * (3 * K - 1)]):
+                p[f"Dense_{l}"] = {
+                    "kernel": _lecun(rng, fan_in, w),
+                    "bias": (bias_scale * rng.standard_normal(w)).astype(np.float32),
+                }
+                fan_in = w
+            params[key] = p
+            stats[key] = {
+                "BatchNorm_0": {
+                    "mean": (0.2 * rng.standard_normal(DC)).astype(np.float32),
+                    "var": (1 + 0.5 * rng.uniform(size=DC)).astype(np.float32),
+                }
+            }
+    return spec, {"params": {"bijector": params}, "batch_stats": {"bijector": stats}}
+
+
+def make_case(name, N=4096, seed=0, bias_scale=0.3):
+    """Seeded case: x ~ N(0, I), c ~ N(0, I); ShiftBounds stats from a separate
+    train-mode pass (margin 0.1) so some eval rows clip."""
+    from oracle import zf_oracle as O
+
+    cfg = dict(CONFIGS[name])
+    rng = np.random.default_rng(seed)
+    spec, variables = make_variables(cfg, rng, bias_scale)
+    xs = rng.standard_normal((4096, cfg["D"])).astype(np.float32)
+    _, _, sb = O.shift_bounds_forward(spec["bijectors"][0], {}, xs, train=True)
+    variables["batch_stats"]["bijector"]["bijectors_0"] = {k: np.asarray(v, np.float32) for k, v in sb.items()}
+    x = rng.standard_normal((N, cfg["D"])).astype(np.float32)
+    c = rng.standard_normal((N, cfg["C"])).astype(np.float32) if cfg["C"] else None
+    model = {"bijector": spec, "latent": {"type": cfg["latent"]}}
+    return {"cfg": cfg, "model": model, "variables": variables, "x": x, "c": c, "name": name}
+
+
+def build_flow(cfg):
+    """The zenflow_amd module matching ``chain_spec(cfg)``."""
+    import zenflow_amd as zf
+    from zenflow_amd import bijectors as bi
+    from zenflow_amd import distributions as dist
+
+    latent = {
+        "normal": dist.Normal,
+        "beta": dist.Beta,
+        "truncated_normal": dist.TruncatedNormal,
+        "uniform": dist.Uniform,
+    }[cfg["latent"]]()
+    spec = chain_spec(cfg)
+    mods = []
+    for b in spec["bijectors"]:
+        if b["type"] == "shift_bounds":
+            mods.append(bi.ShiftBounds(margin=b["margin"], bounds=b["bounds"]))
+        elif b["type"] == "nsc":
+            mods.append(bi.NeuralSplineCoupling(knots=b["knots"], layers=tuple(b["layers"])))
+        else:
+            mods.append(bi.Roll(b["shift"]))
+    return zf.Flow(bi.Chain(mods), latent=latent)

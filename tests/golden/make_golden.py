@@ -1,0 +1,55 @@
+"""Generate the committed golden fixtures under tests/golden/ from the fp32 CPU
+oracle (itself pinned by tests/test_oracle_kats.py against the reference's
+known-answer tests).  Run: ``python tests/golden/make_golden.py``.
+
+* rqs_K{8,16,32}.npz — utils.rational_quadratic_spline_{forward,inverse}
+  inputs/outputs (M=2048, N=2, logits with sigma in {0.1, 1, 3}, x incl. OOB);
+* flow_<cfg>.npz — Flow.log_prob for BASELINE configs at small N, with the
+  case metadata (inputs are regenerated from the seed and checked equal).
+"""
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from oracle import zf_oracle as O  # noqa: E402
+from tests.flowcases import make_case  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+
+
+def rqs_fixtures():
+    for K in (8, 16, 32):
+        rng = np.random.default_rng(K)
+        M, N = 512, 2
+        sig = rng.choice([0.1, 1.0, 3.0], size=(M, 1, 1)).astype(np.float32)
+        dx = (sig * rng.standard_normal((M, N, K))).astype(np.float32)
+        dy = (sig * rng.standard_normal((M, N, K))).astype(np.float32)
+        sl = (sig * rng.standard_normal((M, N, K - 1))).astype(np.float32)
+        dx, dy, sl = O.normalize_spline_params(dx, dy, sl)
+        x = rng.uniform(-0.1, 1.1, size=(M, N)).astype(np.float32)
+        y, ld = O.rqs_forward(x, dx, dy, sl)
+        xi = O.rqs_inverse(y, dx, dy, sl)
+        np.savez_compressed(OUT / f"rqs_K{K}.npz", x=x, dx=dx, dy=dy, slope=sl, y=y, log_det=ld, x_inv=xi)
+
+
+def flow_fixtures():
+    for name, N, seed in [("cfg1", 1024, 101), ("cfg2", 1024, 102), ("cfg4", 1024, 104), ("cfg5", 256, 105)]:
+        case = make_case(name, N=N, seed=seed)
+        lp, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"])
+        lp64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float64)
+        meta = json.dumps({"name": name, "N": N, "seed": seed})
+        np.savez_compressed(OUT / f"flow_{name}.npz", x=case["x"], log_prob=lp, log_prob64=lp64,
+                            meta=np.array(meta))
+
+
+if __name__ == "__main__":
+    rqs_fixtures()
+    flow_fixtures()
+    for f in sorted(OUT.glob("*.npz")):
+        print(f.name, f.stat().st_size)

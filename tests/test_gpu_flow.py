@@ -1,0 +1,177 @@
+"""Fused flow kernel parity: zenflow_amd Flow/Chain (one HIP launch) vs the oracle,
+at every BASELINE.json config shape, plus full-size properties.  Needs the GPU.
+
+Tolerance (north star: 1e-5 relative fp32): per sample
+|gpu - oracle32| <= 1e-5 * max(1, |oracle64|), and the GPU's error against the
+fp64 oracle must not exceed 2x the fp32 oracle's own error + 2e-6 (both are
+fp32 evaluations of the same graph with different rounding orders)."""
+
+import numpy as np
+import pytest
+from numpy.testing import assert_allclose
+
+from oracle import zf_oracle as O
+from tests.flowcases import CONFIGS, build_flow, make_case
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+REL = 1e-5
+
+
+def gpu_log_prob(case):
+    flow = build_flow(case["cfg"])
+    return flow.apply(case["variables"], case["x"], case["c"])
+
+
+def check_lp(lp, case, tag=""):
+    ref32, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float32)
+    ref64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float64)
+    assert lp.shape == ref32.shape and lp.dtype == np.float32
+    scale = np.maximum(1.0, np.abs(ref64))
+    fin32 = np.isfinite(ref32) & (np.abs(ref32) < 1e38)
+    fin_gpu = np.isfinite(lp) & (np.abs(lp) < 1e38)
+    # A row can only disagree on finiteness through the idx == K sliver (an
+    # fp32 knot-sum rounding); those must be rare.
+    mismatch = fin32 != fin_gpu
+    assert mismatch.mean() <= 1e-3, f"{tag}: {mismatch.sum()} finiteness mismatches"
+    both = fin32 & fin_gpu
+    allow = REL * scale[both] + 2 * np.abs(ref32[both].astype(np.float64) - ref64[both])
+    diff = np.abs(lp[both].astype(np.float64) - ref32[both])
+    err = diff / scale[both]
+    assert np.all(diff <= allow), f"{tag}: {np.sum(diff > allow)} rows over tolerance, max rel err {err.max():.3g}"
+    e_gpu = np.abs(lp[both].astype(np.float64) - ref64[both]) / scale[both]
+    e_o32 = np.abs(ref32[both].astype(np.float64) - ref64[both]) / scale[both]
+    assert e_gpu.max() <= 2 * e_o32.max() + 2e-6, f"{tag}: gpu {e_gpu.max():.3g} vs fp32 oracle {e_o32.max():.3g}"
+    return err.max()
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep"])
+@pytest.mark.parametrize("N", [1, 1000, 4096])
+def test_log_prob_parity(name, N):
+    case = make_case(name, N=N, seed=11)
+    check_lp(gpu_log_prob(case), case, f"{name}/N={N}")
+
+
+def test_log_prob_parity_cfg5():
+    case = make_case("cfg5", N=2048, seed=12)
+    check_lp(gpu_log_prob(case), case, "cfg5")
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5"])
+def test_inverse_parity(name):
+    case = make_case(name, N=2000, seed=13)
+    rng = np.random.default_rng(7)
+    z = (0.5 + 0.1 * rng.standard_normal(case["x"].shape)).astype(F32)
+    flow = build_flow(case["cfg"])
+    bij = flow.bijector
+    sub = {k: v["bijector"] for k, v in case["variables"].items()}
+    x = bij.apply(sub, z, case["c"], method="inverse")
+    ref = O.flow_inverse(case["model"], case["variables"], z, case["c"])
+    fin = np.isfinite(ref)
+    assert np.mean(fin != np.isfinite(x)) <= 1e-3
+    both = fin & np.isfinite(x)
+    assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
+
+
+@pytest.mark.parametrize("name", ["cfg2", "odd"])
+def test_chain_forward_parity(name):
+    """Chain.__call__ (y, log_det) vs the oracle's chain."""
+    case = make_case(name, N=3000, seed=14)
+    flow = build_flow(case["cfg"])
+    sub = {k: v["bijector"] for k, v in case["variables"].items()}
+    y, ld = flow.bijector.apply(sub, case["x"], case["c"])
+    c = case["c"]
+    yr, ldr, _ = O.chain_forward(case["model"]["bijector"], sub["params"], sub["batch_stats"],
+                                 case["x"], c, False, np.float32)
+    fin = np.isfinite(ldr)
+    assert np.mean(fin != np.isfinite(ld)) <= 1e-3
+    both = fin & np.isfinite(ld)
+    assert_allclose(y[both], yr[both], rtol=2e-5, atol=2e-6)
+    assert_allclose(ld[both], ldr[both], rtol=REL, atol=REL)
+
+
+def test_golden_flows():
+    """Committed golden fixtures (tests/golden/make_golden.py)."""
+    import json
+    from pathlib import Path
+
+    g = Path(__file__).parent / "golden"
+    for f in sorted(g.glob("flow_*.npz")):
+        d = np.load(f)
+        meta = json.loads(str(d["meta"]))
+        case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
+        assert np.array_equal(case["x"], d["x"]), f"{f.name}: input generation drifted"
+        lp = gpu_log_prob(case)
+        ref, ref64 = d["log_prob"], d["log_prob64"]
+        fin = np.isfinite(ref) & np.isfinite(lp) & np.isfinite(ref64)
+        assert np.mean(np.isfinite(ref) != np.isfinite(lp)) <= 1e-3
+        allow = REL * np.maximum(1.0, np.abs(ref64[fin])) + 2 * np.abs(ref[fin] - ref64[fin])
+        assert np.all(np.abs(lp[fin].astype(np.float64) - ref[fin]) <= allow), f.name
+
+
+# --- full-size (batch 2^20) size-independent properties ---------------------------
+
+
+def _bound(case):
+    import zenflow_amd as zf
+
+    flow = build_flow(case["cfg"])
+    return flow, flow.bind(case["variables"], case["cfg"]["D"], case["cfg"]["C"])
+
+
+def test_full_size_nll_and_roundtrip():
+    """cfg2 at N = 2^20: NLL reduce == fp64 sum of the per-sample log_probs;
+    inverse(forward(x)) == x; a 4096-row sample matches the oracle."""
+    from zenflow_amd._lib import DeviceArray
+
+    N = 1 << 20
+    case = make_case("cfg2", N=N, seed=21)
+    flow, bf = _bound(case)
+    xd = DeviceArray.from_numpy(case["x"])
+    nll = DeviceArray((1,), np.float64)
+    lp = bf.log_prob(xd, nll_sum=nll).numpy()
+    s = nll.numpy()[0]
+    lp64 = lp.astype(np.float64)
+    assert np.isfinite(lp).mean() > 0.999
+    assert abs(s - lp64.sum()) <= 1e-9 * max(1.0, abs(s))
+    # spot check against the oracle on a strided subset
+    idx = np.arange(0, N, N // 4096)
+    sub = dict(case, x=case["x"][idx])
+    ref, _ = O.flow_log_prob(case["model"], case["variables"], sub["x"], None)
+    fin = np.isfinite(ref) & np.isfinite(lp[idx])
+    assert (np.abs(lp[idx][fin] - ref[fin]) / np.maximum(1, np.abs(ref[fin]))).max() <= REL
+    # round trip through the bijector (x -> z -> x); clipped ShiftBounds rows excluded
+    y, ld = bf.forward(xd)
+    xr = bf.inverse(y).numpy()
+    yh = y.numpy()
+    inside = np.all((yh > 1e-3) & (yh < 1 - 1e-3), axis=1) & np.all(np.isfinite(xr), axis=1)
+    assert inside.mean() > 0.5
+    assert_allclose(xr[inside], case["x"][inside], rtol=1e-4, atol=1e-4)
+
+
+def test_determinism():
+    from zenflow_amd._lib import DeviceArray
+
+    case = make_case("cfg2", N=50000, seed=22)
+    _, bf = _bound(case)
+    xd = DeviceArray.from_numpy(case["x"])
+    a = bf.log_prob(xd).numpy()
+    b = bf.log_prob(xd).numpy()
+    assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_edge_inputs():
+    """NaN rows -> -inf (flow.py:47), huge inputs clip, empty batch."""
+    case = make_case("cfg2", N=64, seed=23)
+    x = case["x"].copy()
+    x[3, 1] = np.nan
+    x[5] = 1e30
+    x[6] = -1e30
+    case["x"] = x
+    lp = gpu_log_prob(case)
+    ref, _ = O.flow_log_prob(case["model"], case["variables"], x, None)
+    assert lp[3] == -np.inf and ref[3] == -np.inf
+    fin = np.isfinite(ref)
+    assert_allclose(lp[fin], ref[fin], rtol=REL, atol=REL)
+    case["x"] = np.zeros((0, 4), F32)
+    assert gpu_log_prob(case).shape == (0,)

@@ -1,0 +1,119 @@
+"""Host-side logic of the API mirror (no GPU): module construction, FLAX
+variable layout, errors, op flattening, sharding."""
+
+import numpy as np
+import pytest
+
+import zenflow_amd as zf
+import zenflow_amd.bijectors as bi
+import zenflow_amd.distributions as dist
+from zenflow_amd.engine import flatten, sb_modes
+from zenflow_amd import _lib as L
+from zenflow_amd.dist import shard_rows
+from zenflow_amd.random import PRNGKey
+
+
+def test_bijector_is_abstract():
+    """test_bijectors.py:13-32."""
+    with pytest.raises(TypeError):
+        bi.Bijector()
+
+    class Foo(bi.Bijector):
+        def __call__(self, x, c, train=False):
+            return super().__call__(x, c, train)
+
+        def inverse(self, x, c):
+            return super().inverse(x, c)
+
+    foo = Foo()
+    x = np.array((1, 2, 3))
+    with pytest.raises(NotImplementedError):
+        foo(x, x)
+    with pytest.raises(NotImplementedError):
+        foo.inverse(x, x)
+
+
+def test_rolling_spline_coupling_structure():
+    """bijectors.py:417-423: SB, (NSC, Roll) x (dim-1), NSC."""
+    rsc = bi.rolling_spline_coupling(4, knots=16)
+    kinds = [type(b).__name__ for b in rsc]
+    assert kinds == ["ShiftBounds"] + ["NeuralSplineCoupling", "Roll"] * 3 + ["NeuralSplineCoupling"]
+    with pytest.raises(ValueError):
+        bi.rolling_spline_coupling(1)
+    pre = bi.rolling_spline_coupling(2, preprocessing=[bi.Roll()])
+    assert type(pre[0]).__name__ == "Roll" and len(pre) == 4
+
+
+def test_flax_variable_layout():
+    """Flow(rolling_spline_coupling(D)) variables match FLAX naming and shapes
+    (examples/deep_set.ipynb:466-485, tests/test_bijectors.py:201)."""
+    flow = zf.Flow(bi.rolling_spline_coupling(2, knots=16), latent=dist.Beta())
+    x = np.zeros((5, 2), np.float32)
+    c = np.zeros((5, 8), np.float32)
+    v = flow.init(PRNGKey(0), x, c)
+    p = v["params"]["bijector"]
+    assert sorted(p) == ["bijectors_1", "bijectors_3"]
+    nsc = p["bijectors_1"]
+    assert sorted(nsc) == ["BatchNorm_0", "Dense_0", "Dense_1", "Dense_2"]
+    assert nsc["Dense_0"]["kernel"].shape == (9, 128)
+    assert nsc["Dense_2"]["kernel"].shape == (128, 47)
+    assert nsc["BatchNorm_0"]["scale"].shape == (9,)
+    s = v["batch_stats"]["bijector"]
+    assert s["bijectors_0"]["xmin_0"].shape == (1,) and np.isinf(s["bijectors_0"]["xmin_0"]).all()
+    assert s["bijectors_1"]["BatchNorm_0"]["var"].shape == (9,)
+    assert flow.latent.dim == 2
+
+
+def test_lecun_normal_init_statistics():
+    flow = zf.Flow(bi.rolling_spline_coupling(4))
+    v = flow.init(PRNGKey(1), np.zeros((1, 4)))
+    k = v["params"]["bijector"]["bijectors_1"]["Dense_1"]["kernel"]
+    assert np.abs(k).max() <= 2 * np.sqrt(1 / 128) / 0.87962566 + 1e-6
+    assert abs(k.std() - np.sqrt(1 / 128)) < 0.01
+
+
+def test_shift_bounds_errors():
+    with pytest.raises(ValueError):
+        bi.ShiftBounds(margin=-0.5)
+    with pytest.raises(ValueError):
+        bi.ShiftBounds(margin=1.5)
+    with pytest.raises(ValueError):
+        bi.ShiftBounds(bounds=[(3, None, 1)]).init(PRNGKey(0), np.zeros((2, 2)), None)
+    modes = sb_modes(bi.ShiftBounds(bounds=[(0, -1, 1), (1, 10, None), (2, None, 1), (3, np.inf, None)]), 5)
+    assert [m for m, _, _ in modes] == [L.ZF_SB_BOTH, L.ZF_SB_LOWER, L.ZF_SB_UPPER, L.ZF_SB_NONE, L.ZF_SB_NONE]
+
+
+def test_flatten_nested_chain():
+    inner = bi.chain(bi.NeuralSplineCoupling(), bi.Roll())
+    outer = bi.Chain([bi.ShiftBounds(), inner, bi.NeuralSplineCoupling()])
+    ops = flatten(outer)
+    assert [o.kind for o in ops] == [L.ZF_OP_SHIFT_BOUNDS, L.ZF_OP_NSC, L.ZF_OP_ROLL, L.ZF_OP_NSC]
+    assert ops[1].path == ("bijectors_1", "bijectors_0")
+
+
+def test_distribution_errors_and_repr():
+    with pytest.raises(ValueError):
+        dist.Beta(0.5)
+    assert repr(dist.Beta()) == "Beta(peakness=12.0)"
+    assert repr(dist.Normal()) == "Normal()"
+
+
+def test_apply_outside_scope_raises():
+    nsc = bi.NeuralSplineCoupling()
+    with pytest.raises(RuntimeError, match="outside of init/apply"):
+        nsc(np.zeros((2, 2)))
+
+
+def test_train_is_out_of_scope():
+    with pytest.raises(NotImplementedError):
+        zf.train(None, None, None)
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (1 << 20, 8), (5, 8), (0, 2)])
+def test_shard_rows(n, world):
+    spans = [shard_rows(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,67 @@
+"""Build libzenflow_amd.so in-tree with hipcc for gfx950 (MI355X).
+
+``python -m zenflow_amd.build`` (or ``__graft_entry__.build()``).  The output
+lands next to this file so the built library travels with the repository
+snapshot to the GPU box.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+INCLUDE = HERE.parent / "include"
+LIB = HERE / "libzenflow_amd.so"
+ARCH = os.environ.get("ZF_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["zf_runtime.hip", "zf_rqs.hip", "zf_flow.hip", "zf_stats.hip", "zf_rccl.hip"]
+HEADERS = ["zf_internal.h", "zf_spline.h"]
+
+FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-variable",
+    "-Wno-unused-result",
+    "-I/opt/rocm/include",
+    f"-I{INCLUDE}",
+]
+
+
+def _fingerprint() -> str:
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        h.update((CSRC / f).read_bytes())
+    h.update((INCLUDE / "zenflow_amd.h").read_bytes())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    """Compile every HIP source into one shared library (skip if up to date)."""
+    stamp = HERE / ".libzenflow_amd.sha256"
+    fp = _fingerprint()
+    if not force and LIB.exists() and stamp.exists() and stamp.read_text() == fp:
+        return LIB
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, *FLAGS, "-o", str(tmp), *[str(CSRC / s) for s in SOURCES], "-ldl"]
+    if verbose:
+        print("[zenflow_amd.build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    stamp.write_text(fp)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,806 @@
+// Fused flow kernel: one launch runs a whole zenflow bijector chain
+// (ShiftBounds -> [NeuralSplineCoupling, Roll]* -> NeuralSplineCoupling) and
+// the latent log_prob epilogue for a tile of samples, keeping every
+// intermediate on chip.  Reference call stack:
+//   Flow.__call__ (flow.py:22-48) -> Chain.__call__ (bijectors.py:103-111)
+//   -> ShiftBounds (:163-273) / Roll (:288-297) / NeuralSplineCoupling (:359-371)
+//   -> conditioner MLP (:329-357) + normalize_spline_params + RQ spline (utils.py).
+//
+// Execution model (DESIGN.md §Fused kernel):
+//   * one wave64 owns a tile of 32 samples; a 256-thread block = 4 independent
+//     waves = 128 samples (no inter-wave sync in the op loop);
+//   * conditioner GEMMs on fp32 MFMA v_mfma_f32_32x32x2_f32 (exact f32 fma
+//     chain): weights are the A operand (out-unit x in-unit), activations the B
+//     operand (in-unit x sample).  A layer's accumulator tile (unit rows in
+//     registers, sample on the lane) is directly the B operand of the next
+//     layer -> hidden activations never leave registers;
+//   * weights are pre-packed in MFMA fragment order and streamed from L2 with
+//     one dwordx4 per lane per 4 MFMAs (every wave reads the same bytes);
+//   * the last layer's 32-row output tiles go through a per-wave LDS ring
+//     (lane = sample, conflict-free), where one lane per (sample, dim) runs
+//     normalize_spline_params + bin search + RQ spline + log-det in registers;
+//   * per-sample state (D floats) lives in LDS; Roll is an index rotation.
+#include "zf_internal.h"
+#include "zf_spline.h"
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace zf {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWaves = 4;               // waves per block
+constexpr int kTile = 32;               // samples per wave
+constexpr int kBlockRows = kWaves * kTile;
+constexpr int kMaxOps = 64;
+
+struct DevOp {
+  int kind, shift, K, S;
+  int n_hidden, dt, dc, DC;
+  int KS0, T_last, nslot_mask, act;
+  long long w[17];
+  long long b[17];
+  long long bn;
+  long long sb;
+};
+
+struct DevFlow {
+  int D, C, latent, n_ops;
+  int HP, nslot, per_wave, pad;
+  float lat_c0, lat_c1, lat_c2, lat_c3;
+  DevOp ops[kMaxOps];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave execute in order; this only stops the compiler from
+  // moving LDS accesses across the exchange point.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float swish(float v) {
+  // flax.linen.swish = x * sigmoid(x) (bijectors.py:319)
+  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.44269504f));
+}
+
+__device__ __forceinline__ int pmod(int a, int m) {
+  int r = a % m;
+  return r < 0 ? r + m : r;
+}
+
+// Raw conditioner outputs of one (sample, transformed dim) in the LDS ring:
+// row q of the last layer lives at slot (q>>5)&mask, row q&31, column s.
+struct RingParams {
+  const float* ring;  // wave ring base + s
+  int base;           // d * S
+  int K, mask;
+  float sx, sy, c, norm;
+  __device__ __forceinline__ float at(int q) const {
+    return ring[(((q >> 5) & mask) << 10) + ((q & 31) << 5)];
+  }
+  // softmax_with_threshold (utils.py:23-34); squareplus values were stored in place
+  __device__ __forceinline__ float w(int j) const { return (at(base + j) / sx + c) / norm; }
+  __device__ __forceinline__ float h(int j) const { return (at(base + K + j) / sy + c) / norm; }
+  __device__ __forceinline__ float d(int j) const { return squareplus(at(base + 2 * K + j)); }
+};
+
+template <int HP, bool INV>
+__global__ __launch_bounds__(kWaves * 64) void flow_kernel(
+    const DevFlow* __restrict__ F, const float* __restrict__ blob, const float* __restrict__ xin,
+    const float* __restrict__ cin, float* __restrict__ y_out, const float* __restrict__ ld_in,
+    float* __restrict__ ld_out, float* __restrict__ lp_out, double* __restrict__ block_partial,
+    int op_begin, int op_end, long long N) {
+  constexpr int T = HP / 32;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double s_part[kWaves];
+
+  const int D = F->D;
+  const int C = F->C;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int s = lane & 31;
+  const int hh = lane >> 5;
+  float* xs = lds + wave * F->per_wave;  // state [D][32]
+  float* ring = xs + 32 * D;            // [nslot][32 rows][32 samples]
+  const long long row = ((long long)blockIdx.x * kWaves + wave) * kTile + s;
+  const bool valid = row < N;
+
+  for (int d = hh; d < D; d += 2) xs[d * 32 + s] = valid ? xin[row * D + d] : 0.f;
+  float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
+  int rot = 0;  // logical dim j is stored in column (j + rot) mod D
+  wave_lds_sync();
+
+  const int nq = op_end - op_begin;
+  for (int q = 0; q < nq; ++q) {
+    const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+    const DevOp& op = F->ops[oi];
+    const int kind = op.kind;
+    if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
+      rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
+    } else if (kind == ZF_OP_SHIFT_BOUNDS) {
+      const float* sb = blob + op.sb;
+      if (!INV) {  // bijectors.py:181-208 (eval branch of :261-273)
+        float ldsb = 0.f;
+        for (int i = 0; i < D; ++i) {
+          const int p = pmod(i + rot, D);
+          const float v = xs[p * 32 + s];
+          const int mode = (int)sb[8 * i];
+          const float a = sb[8 * i + 1], b = sb[8 * i + 2], xmin = sb[8 * i + 3];
+          const float mul = sb[8 * i + 5], logmul = sb[8 * i + 6];
+          float z, l;
+          if (mode == ZF_SB_BOTH) {  // :187-192
+            z = (v - a) * mul;
+            l = logmul;
+          } else {
+            float t = v;
+            if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);  // safe_log :430
+            if (mode == ZF_SB_UPPER) t = logf((b - v) + 1.17549435e-38f);
+            const float zr = (t - xmin) * mul;
+            z = (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);  // :272 clip
+            l = (mode == ZF_SB_NONE) ? logmul : logmul - t;    // :197, :202
+          }
+          ldsb = ldsb + l;
+          if (hh == 0) xs[p * 32 + s] = z;
+        }
+        ld = ld + ldsb;
+      } else {  // bijectors.py:210-240
+        for (int i = 0; i < D; ++i) {
+          const int p = pmod(i + rot, D);
+          const float zv = xs[p * 32 + s];
+          const int mode = (int)sb[8 * i];
+          const float a = sb[8 * i + 1], b = sb[8 * i + 2];
+          const float xmin = sb[8 * i + 3], xmax = sb[8 * i + 4];
+          float xv;
+          if (mode == ZF_SB_BOTH) {
+            xv = zv * b + (1.f - zv) * a;
+          } else {
+            const float t = zv * xmax + (1.f - zv) * xmin;
+            xv = (mode == ZF_SB_LOWER) ? expf(t) + a : (mode == ZF_SB_UPPER ? b - expf(t) : t);
+          }
+          if (hh == 0) xs[p * 32 + s] = xv;
+        }
+      }
+      wave_lds_sync();
+    } else {  // ZF_OP_NSC, bijectors.py:329-371
+      const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
+      const int DCp = 2 * KS0;
+      const float* bn = blob + op.bn;
+      floatx16 hb[T];
+#pragma unroll
+      for (int o = 0; o < T; ++o) hb[o] = floatx16{0};
+      // Layer 0: u = BatchNorm(hstack(xc, c)) (:341-342), one MFMA k-step per 2 inputs.
+      for (int ks = 0; ks < KS0; ++ks) {
+        const int k = 2 * ks + hh;
+        float v = 0.f;
+        if (k < dc) v = xs[pmod(dt + k + rot, D) * 32 + s];
+        else if (k < DC) v = valid ? cin[row * C + (k - dc)] : 0.f;
+        const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
+        const float* w0 = blob + op.w[0] + ks * 64 + lane;
+#pragma unroll
+        for (int o = 0; o < T; ++o)
+          hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
+      }
+      {
+        const float* b0 = blob + op.b[0] + hh * 16;
+#pragma unroll
+        for (int o = 0; o < T; ++o)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + b0[o * 32 + r]);
+      }
+      // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.
+      for (int l = 1; l < op.n_hidden; ++l) {
+        const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[l]) + lane;
+        const float* bl = blob + op.b[l] + hh * 16;
+        floatx16 ho[T];
+#pragma unroll
+        for (int o = 0; o < T; ++o) {
+          floatx16 acc = floatx16{0};
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const floatx4 w = wl[((o * T + t) * 4 + r4) * 64];
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[e], hb[t][4 * r4 + e], acc, 0, 0, 0);
+            }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = swish(acc[r] + bl[o * 32 + r]);
+          ho[o] = acc;
+        }
+#pragma unroll
+        for (int o = 0; o < T; ++o) hb[o] = ho[o];
+      }
+      // Last Dense (:346) -> (N, dt, 3K-1) params (:347), tile by tile through the ring.
+      const int K = op.K, S = op.S, mask = op.nslot_mask;
+      const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[op.n_hidden]) + lane;
+      const float* bl = blob + op.b[op.n_hidden] + hh * 16;
+      // utils.py:32-34: c and 1 + c*n are Python floats (fp64), rounded to fp32 on use
+      const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
+      const float cth = (float)c64;
+      const float norm = (float)(1.0 + c64 * (double)K);
+      int next_d = 0;
+      float ldc = 0.f;
+      for (int o = 0; o < op.T_last; ++o) {
+        floatx16 acc = floatx16{0};
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const floatx4 w = wl[((o * T + t) * 4 + r4) * 64];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[e], hb[t][4 * r4 + e], acc, 0, 0, 0);
+          }
+        float* slot = ring + ((o & mask) << 10) + s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          slot[rr * 32] = acc[r] + bl[o * 32 + r];
+        }
+        wave_lds_sync();
+        // Run the spline for the next pair of transformed dims once all of
+        // their 2*S parameter rows are in the ring: lanes 0-31 take dim
+        // next_d, lanes 32-63 dim next_d+1.
+        while (next_d < dt) {
+          const int end = (next_d + 2 < dt) ? next_d + 2 : dt;
+          if (end * S > (o + 1) * 32) break;
+          const int d = next_d + hh;
+          float ldv = 0.f;
+          if (d < end) {
+            RingParams p;
+            p.ring = ring + s;
+            p.base = d * S;
+            p.K = K;
+            p.mask = mask;
+            p.c = cth;
+            p.norm = norm;
+            float* rp = ring + s;
+            float sx = 0.f, sy = 0.f;
+            for (int j = 0; j < K; ++j) {  // squareplus in place + sums (utils.py:30-33)
+              const int qx = p.base + j, qy = p.base + K + j;
+              float* ax = rp + (((qx >> 5) & mask) << 10) + ((qx & 31) << 5);
+              float* ay = rp + (((qy >> 5) & mask) << 10) + ((qy & 31) << 5);
+              const float vx = squareplus(*ax), vy = squareplus(*ay);
+              *ax = vx;
+              *ay = vy;
+              sx = sx + vx;
+              sy = sy + vy;
+            }
+            p.sx = sx;
+            p.sy = sy;
+            float* xp = xs + pmod(d + rot, D) * 32 + s;
+            const float xv = *xp;
+            const RqsBin bin = rqs_bin<!INV>(xv, K, p);
+            if (!INV) {
+              float yv, l;
+              rqs_forward_eval(xv, bin, yv, l);
+              *xp = yv;
+              ldv = l;
+            } else {
+              *xp = rqs_inverse_eval(xv, bin);
+            }
+          }
+          wave_lds_sync();
+          if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139)
+            const float other = __shfl_xor(ldv, 32);
+            const float first = hh == 0 ? ldv : other;
+            const float second = hh == 0 ? other : ldv;
+            ldc = ldc + first;
+            if (end - next_d == 2) ldc = ldc + second;
+          }
+          next_d += 2;
+        }
+      }
+      if (!INV) ld = ld + ldc;  // Chain: log_det += ld (bijectors.py:110)
+    }
+  }
+
+  // ---- epilogue -----------------------------------------------------------
+  if (lp_out != nullptr) {
+    // latent.log_prob(z) (distributions.py:16-33) + log_det (flow.py:46)
+    const int lt = F->latent;
+    const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
+    float lat = 0.f;
+    for (int j = 0; j < D; ++j) {
+      const float v = xs[pmod(j + rot, D) * 32 + s];
+      float t;
+      if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
+        // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
+        const float dv = v - 0.5f;
+        t = (c0 + (dv * dv) / c1) / -2.0f;
+        if (lt == ZF_LATENT_TRUNCNORM) {  // - log mass; -inf outside [-5, 5] sigma
+          t = t - c2;
+          const float xsd = dv / 0.1f;
+          if (xsd < -5.f || xsd > 5.f) t = -INFINITY;
+        }
+      } else if (lt == ZF_LATENT_BETA) {
+        // -betaln(a,a) + xlogy(a-1, x) + xlog1py(a-1, -x); -inf outside [0, 1]
+        const float l1 = (c1 == 0.f) ? 0.f : c1 * logf(v);
+        const float l2 = (c1 == 0.f) ? 0.f : c1 * log1pf(-v);
+        t = c0 + (l1 + l2);
+        if (v > 1.f || v < 0.f) t = -INFINITY;
+      } else {  // uniform
+        t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
+      }
+      lat = lat + t;
+    }
+    float lp = lat + ld;
+    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): +-inf -> +-max finite
+    if (lp != lp) lp = -INFINITY;
+    else if (lp == INFINITY) lp = 3.40282347e38f;
+    else if (lp == -INFINITY) lp = -3.40282347e38f;
+    if (valid && hh == 0) lp_out[row] = lp;
+    if (block_partial != nullptr) {
+      double v = (valid && hh == 0) ? (double)lp : 0.0;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      if (lane == 0) s_part[wave] = v;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double acc = 0.0;
+        for (int w = 0; w < kWaves; ++w) acc += s_part[w];
+        block_partial[blockIdx.x] = acc;
+      }
+    }
+  }
+  if (y_out != nullptr && valid) {
+    for (int j = hh; j < D; j += 2) y_out[row * D + j] = xs[pmod(j + rot, D) * 32 + s];
+  }
+  if (ld_out != nullptr && valid && hh == 0) ld_out[row] = ld;
+}
+
+// Deterministic fixed-order sum of per-block partials -> out[0].
+__global__ __launch_bounds__(256) void reduce_partials(const double* __restrict__ part, long long n,
+                                                       double* __restrict__ out) {
+  __shared__ double sm[256];
+  double acc = 0.0;
+  for (long long i = threadIdx.x; i < n; i += 256) acc += part[i];
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if ((int)threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sm[0];
+}
+
+// ---------------------------------------------------------------------------
+// Host side: planning, packing, launches.
+// ---------------------------------------------------------------------------
+
+int round_up(int a, int m) { return (a + m - 1) / m * m; }
+int64_t round_up64(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+struct OpGeom {
+  int dt, dc, DC, K, S, OUT, KS0, T_last, nslot;
+};
+
+OpGeom nsc_geom(const zf_flow_desc* desc, const zf_op_desc& op) {
+  OpGeom g;
+  const int D = desc->dim;
+  g.dt = D / 2;
+  g.dc = D - g.dt;
+  g.DC = g.dc + desc->cond_dim;
+  g.K = op.knots;
+  g.S = 3 * g.K - 1;
+  g.OUT = g.dt * g.S;
+  g.KS0 = (g.DC + 1) / 2;
+  g.T_last = (g.OUT + 31) / 32;
+  const int span = (g.dt >= 2 ? 2 * g.S : g.S);
+  int need = (span + 31) / 32 + 1;
+  if (need > g.T_last) need = g.T_last;
+  g.nslot = next_pow2(need);
+  return g;
+}
+
+int hidden_pad_of(const zf_flow_desc* desc) {
+  int hmax = 0;
+  for (int i = 0; i < desc->n_ops; ++i) {
+    const zf_op_desc& op = desc->ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    for (int l = 0; l < op.n_hidden; ++l) hmax = op.hidden[l] > hmax ? op.hidden[l] : hmax;
+  }
+  if (hmax == 0) return 32;
+  int hp = 32;
+  while (hp < hmax) hp <<= 1;  // instantiated tile counts: 1, 2, 4, 8
+  return hp;
+}
+
+int validate(const zf_flow_desc* desc) {
+  if (!desc) return einval("desc is NULL");
+  if (desc->dim < 1 || desc->dim > 64) return einval("dim %d out of range [1, 64]", desc->dim);
+  if (desc->cond_dim < 0 || desc->cond_dim > 64) return einval("cond_dim out of range");
+  if (desc->n_ops < 0 || desc->n_ops > kMaxOps) return einval("n_ops out of range");
+  if (desc->latent < ZF_LATENT_NONE || desc->latent > ZF_LATENT_UNIFORM) return einval("bad latent");
+  for (int i = 0; i < desc->n_ops; ++i) {
+    const zf_op_desc& op = desc->ops[i];
+    if (op.kind == ZF_OP_NSC) {
+      if (desc->dim < 2) return einval("NeuralSplineCoupling needs dim >= 2");
+      if (op.knots < 1 || op.knots > 64) return einval("knots %d out of range [1, 64]", op.knots);
+      if (op.n_hidden < 1 || op.n_hidden > 16) return enotsup("n_hidden must be in [1, 16]");
+      for (int l = 0; l < op.n_hidden; ++l)
+        if (op.hidden[l] < 1 || op.hidden[l] > 256) return enotsup("hidden width must be in [1, 256]");
+      if (op.act != ZF_ACT_SWISH) return enotsup("only the swish activation is implemented");
+    } else if (op.kind != ZF_OP_ROLL && op.kind != ZF_OP_SHIFT_BOUNDS) {
+      return einval("op %d: unknown kind %d", i, op.kind);
+    }
+  }
+  return ZF_OK;
+}
+
+}  // namespace
+}  // namespace zf
+
+struct zf_flow {
+  zf_flow_desc desc;
+  zf::DevFlow host;           // device descriptor (host copy)
+  std::vector<float> natural; // natural blob (host copy, for stat updates)
+  std::vector<float> packed;  // device blob (host copy)
+  zf::DevFlow* d_desc = nullptr;
+  float* d_blob = nullptr;
+  int device = 0;
+};
+
+namespace zf {
+namespace {
+
+// Fill the packed (device) blob from the natural blob.  Layouts: zf_flow.hip
+// header + DESIGN.md §Data layout.
+void pack_nsc_bn(const zf_flow_desc* desc, const zf_op_desc& op, const float* nat, float* dst) {
+  const OpGeom g = nsc_geom(desc, op);
+  const int DCp = 2 * g.KS0;
+  const float* mean = nat + op.off_bn;
+  const float* var = mean + g.DC;
+  const float* scale = var + g.DC;
+  const float* bias = scale + g.DC;
+  for (int k = 0; k < DCp; ++k) {
+    if (k < g.DC) {
+      // flax BatchNorm: mul = rsqrt(var + eps) * scale
+      const float mul = (1.0f / std::sqrt(var[k] + 1e-5f)) * scale[k];
+      dst[k] = mean[k];
+      dst[DCp + k] = mul;
+      dst[2 * DCp + k] = bias[k];
+    } else {
+      dst[k] = dst[DCp + k] = dst[2 * DCp + k] = 0.f;
+    }
+  }
+}
+
+void pack_sb(const zf_flow_desc* desc, const zf_op_desc& op, const float* nat, float* dst) {
+  for (int i = 0; i < desc->dim; ++i) {
+    const float* r = nat + op.off_sb + 8 * i;
+    const int mode = (int)r[0];
+    const float a = r[1], b = r[2], xmin = r[3], xmax = r[4];
+    float mul;
+    if (mode == ZF_SB_BOTH) mul = (float)(1.0 / ((double)b - (double)a));  // :189 (Python floats)
+    else mul = 1.0f / (xmax - xmin);                                        // :265
+    float* o = dst + 8 * i;
+    o[0] = (float)mode; o[1] = a; o[2] = b; o[3] = xmin; o[4] = xmax;
+    o[5] = mul; o[6] = std::log(mul); o[7] = 0.f;
+  }
+}
+
+}  // namespace
+}  // namespace zf
+
+extern "C" {
+
+int zf_flow_plan(zf_flow_desc* desc, int64_t* blob_floats) {
+  int rc = zf::validate(desc);
+  if (rc) return rc;
+  if (!blob_floats) return zf::einval("blob_floats is NULL");
+  int64_t off = 0;
+  for (int i = 0; i < desc->n_ops; ++i) {
+    zf_op_desc& op = desc->ops[i];
+    op.off_bn = op.off_sb = 0;
+    for (int l = 0; l < 17; ++l) op.off_w[l] = op.off_b[l] = 0;
+    if (op.kind == ZF_OP_NSC) {
+      const zf::OpGeom g = zf::nsc_geom(desc, op);
+      op.off_bn = off;
+      off += 4 * g.DC;
+      int in = g.DC;
+      for (int l = 0; l <= op.n_hidden; ++l) {
+        const int out = l < op.n_hidden ? op.hidden[l] : g.OUT;
+        op.off_w[l] = off;
+        off += (int64_t)in * out;
+        op.off_b[l] = off;
+        off += out;
+        in = out;
+      }
+    } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
+      op.off_sb = off;
+      off += 8 * desc->dim;
+    }
+  }
+  *blob_floats = off;
+  return ZF_OK;
+}
+
+int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t blob_floats,
+                   zf_flow_t** handle) {
+  if (!handle) return zf::einval("handle is NULL");
+  *handle = nullptr;
+  zf_flow_desc desc = *desc_in;
+  int64_t need = 0;
+  int rc = zf_flow_plan(&desc, &need);
+  if (rc) return rc;
+  if (blob_floats != need) return zf::einval("blob has %lld floats, plan needs %lld", (long long)blob_floats, (long long)need);
+  if (need > 0 && !blob_host) return zf::einval("blob is NULL");
+
+  zf_flow* h = new zf_flow();
+  h->desc = desc;
+  h->natural.assign(blob_host, blob_host + need);
+  zf::DevFlow& F = h->host;
+  std::memset(&F, 0, sizeof(F));
+  F.D = desc.dim;
+  F.C = desc.cond_dim;
+  F.latent = desc.latent;
+  F.n_ops = desc.n_ops;
+  F.HP = zf::hidden_pad_of(&desc);
+  const int HP = F.HP, T = HP / 32;
+  // Latent constants in fp32, as jax.scipy.stats computes them.
+  {
+    const float s2 = 0.1f * 0.1f;
+    F.lat_c0 = std::log(6.28318530717958647692f * s2);
+    F.lat_c1 = s2;
+    if (desc.latent == ZF_LATENT_BETA) {
+      const double a = desc.latent_param;
+      F.lat_c0 = (float)(-(std::lgamma(a) + std::lgamma(a) - std::lgamma(2.0 * a)));
+      F.lat_c1 = (float)a - 1.0f;
+    } else if (desc.latent == ZF_LATENT_TRUNCNORM) {
+      // _log_gauss_mass(-5, 5) = log1p(-ndtr(-5) - ndtr(-5))
+      const float nd = (float)(0.5 * std::erfc(5.0 / std::sqrt(2.0)));
+      F.lat_c2 = std::log1p(-nd - nd);
+    }
+  }
+  // Packed blob layout.
+  int64_t off = 0;
+  auto take = [&](int64_t n) { const int64_t o = off; off = zf::round_up64(off + n, 4); return o; };
+  int nslot = 1;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    zf::DevOp& d = F.ops[i];
+    d.kind = op.kind;
+    d.shift = op.shift;
+    if (op.kind == ZF_OP_NSC) {
+      const zf::OpGeom g = zf::nsc_geom(&desc, op);
+      d.K = g.K; d.S = g.S; d.n_hidden = op.n_hidden; d.dt = g.dt; d.dc = g.dc; d.DC = g.DC;
+      d.KS0 = g.KS0; d.T_last = g.T_last; d.nslot_mask = g.nslot - 1; d.act = op.act;
+      nslot = g.nslot > nslot ? g.nslot : nslot;
+      d.bn = take(3 * 2 * g.KS0);
+      d.w[0] = take((int64_t)T * g.KS0 * 64);
+      d.b[0] = take((int64_t)T * 32);
+      for (int l = 1; l < op.n_hidden; ++l) {
+        d.w[l] = take((int64_t)T * T * 1024);
+        d.b[l] = take((int64_t)T * 32);
+      }
+      d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
+      d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
+    } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
+      d.sb = take(8 * desc.dim);
+    }
+  }
+  F.nslot = nslot;
+  F.per_wave = zf::round_up(32 * desc.dim, 4) + nslot * 1024;
+  h->packed.assign((size_t)(off > 0 ? off : 4), 0.f);
+  float* P = h->packed.data();
+  const float* nat = h->natural.data();
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    const zf::DevOp& d = F.ops[i];
+    if (op.kind == ZF_OP_SHIFT_BOUNDS) {
+      zf::pack_sb(&desc, op, nat, P + d.sb);
+    } else if (op.kind == ZF_OP_NSC) {
+      const zf::OpGeom g = zf::nsc_geom(&desc, op);
+      zf::pack_nsc_bn(&desc, op, nat, P + d.bn);
+      // layer 0: A fragment of (o, ks): lane l -> W0[k = 2ks + (l>>5)][i = 32o + (l&31)]
+      {
+        const int in = g.DC, out = op.hidden[0];
+        const float* W = nat + op.off_w[0];
+        const float* B = nat + op.off_b[0];
+        for (int o = 0; o < T; ++o)
+          for (int ks = 0; ks < g.KS0; ++ks)
+            for (int l = 0; l < 64; ++l) {
+              const int k = 2 * ks + (l >> 5), ii = 32 * o + (l & 31);
+              P[d.w[0] + ((int64_t)o * g.KS0 + ks) * 64 + l] = (k < in && ii < out) ? W[(int64_t)k * out + ii] : 0.f;
+            }
+        for (int o = 0; o < T; ++o)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int r = 0; r < 16; ++r) {
+              const int ii = 32 * o + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              P[d.b[0] + (o * 2 + hh) * 16 + r] = ii < out ? B[ii] : 0.f;
+            }
+      }
+      // layers 1..n_hidden: fragment (o, t, r4, lane, e) ->
+      //   W[k = 32t + e + 8 r4 + 4 (lane>>5)][i = 32o + (lane&31)]
+      for (int l = 1; l <= op.n_hidden; ++l) {
+        const int in = op.hidden[l - 1];
+        const int out = l < op.n_hidden ? op.hidden[l] : g.OUT;
+        const int To = l < op.n_hidden ? T : g.T_last;
+        const float* W = nat + op.off_w[l];
+        const float* B = nat + op.off_b[l];
+        float* Wp = P + d.w[l];
+        for (int o = 0; o < To; ++o)
+          for (int t = 0; t < T; ++t)
+            for (int r4 = 0; r4 < 4; ++r4)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 4; ++e) {
+                  const int k = 32 * t + e + 8 * r4 + 4 * (ln >> 5);
+                  const int ii = 32 * o + (ln & 31);
+                  Wp[((((int64_t)o * T + t) * 4 + r4) * 64 + ln) * 4 + e] =
+                      (k < in && ii < out) ? W[(int64_t)k * out + ii] : 0.f;
+                }
+        for (int o = 0; o < To; ++o)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int r = 0; r < 16; ++r) {
+              const int ii = 32 * o + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              P[d.b[l] + (o * 2 + hh) * 16 + r] = ii < out ? B[ii] : 0.f;
+            }
+      }
+    }
+  }
+  int rcd = ZF_OK;
+  hipError_t e = hipGetDevice(&h->device);
+  if (e == hipSuccess) e = hipMalloc(&h->d_desc, sizeof(zf::DevFlow));
+  if (e == hipSuccess) e = hipMalloc(&h->d_blob, h->packed.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(h->d_desc, &h->host, sizeof(zf::DevFlow), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(h->d_blob, h->packed.data(), h->packed.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    rcd = zf::hip_status(e, "zf_flow_create");
+    zf_flow_destroy(h);
+    return rcd;
+  }
+  *handle = h;
+  return ZF_OK;
+}
+
+int zf_flow_destroy(zf_flow_t* h) {
+  if (!h) return ZF_OK;
+  if (h->d_desc) (void)hipFree(h->d_desc);
+  if (h->d_blob) (void)hipFree(h->d_blob);
+  delete h;
+  return ZF_OK;
+}
+
+int64_t zf_flow_workspace_bytes(int64_t N) {
+  const int64_t blocks = (N + zf::kBlockRows - 1) / zf::kBlockRows;
+  return zf::round_up64(blocks * 8 + 64, 256);
+}
+
+}  // extern "C"
+
+namespace zf {
+namespace {
+
+template <bool INV>
+int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const float* c, float* y,
+                const float* ld_in, float* ld_out, float* lp, double* part, int64_t N,
+                void* stream) {
+  if (!h) return einval("handle is NULL");
+  if (N < 0) return einval("N < 0");
+  if (op_begin < 0 || op_end > h->host.n_ops || op_begin > op_end) return einval("bad op range");
+  if (N == 0) return ZF_OK;
+  if (!x) return einval("x is NULL");
+  if (h->host.C > 0 && !c) return einval("flow is conditional (C=%d) but c is NULL", h->host.C);
+  const int64_t grid = (N + kBlockRows - 1) / kBlockRows;
+  if (grid > 0x7fffffffLL) return einval("N too large");
+  const size_t lds = sizeof(float) * (size_t)kWaves * h->host.per_wave;
+  if (lds > 160 * 1024 - 64) return enotsup("LDS footprint too large (dim/knots)");
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = (long long)N;
+#define ZF_LAUNCH(HPV)                                                                          \
+  hipLaunchKernelGGL((flow_kernel<HPV, INV>), dim3((unsigned)grid), dim3(kWaves * 64), lds, st, \
+                     h->d_desc, h->d_blob, x, c, y, ld_in, ld_out, lp, part, op_begin, op_end, n)
+  switch (h->host.HP) {
+    case 32: ZF_LAUNCH(32); break;
+    case 64: ZF_LAUNCH(64); break;
+    case 128: ZF_LAUNCH(128); break;
+    case 256: ZF_LAUNCH(256); break;
+    default: return enotsup("hidden width");
+  }
+#undef ZF_LAUNCH
+  ZF_CHECK_LAUNCH("flow_kernel");
+  return ZF_OK;
+}
+
+}  // namespace
+}  // namespace zf
+
+extern "C" {
+
+int zf_flow_log_prob_segment(zf_flow_t* h, int op_begin, int op_end, const float* x,
+                             const float* c, const float* log_det_in, float* log_prob,
+                             double* nll_sum, void* workspace, int64_t N, void* stream) {
+  if (!h) return zf::einval("handle is NULL");
+  if (!log_prob) return zf::einval("log_prob is NULL");
+  if (h->host.latent == ZF_LATENT_NONE) return zf::einval("flow has no latent distribution");
+  if (nll_sum && !workspace) return zf::einval("nll_sum requires a workspace");
+  if (N == 0) {
+    if (nll_sum) ZF_TRY_HIP(hipMemsetAsync(nll_sum, 0, sizeof(double), (hipStream_t)stream));
+    return ZF_OK;
+  }
+  double* part = (double*)workspace;  // per-block partials when a workspace is given
+  int rc = zf::launch_flow<false>(h, op_begin, op_end, x, c, nullptr, log_det_in, nullptr,
+                                  log_prob, part, N, stream);
+  if (rc) return rc;
+  if (nll_sum) return zf_flow_nll_reduce(workspace, N, nll_sum, stream);
+  return ZF_OK;
+}
+
+int zf_flow_nll_reduce(const void* workspace, int64_t N, double* nll_sum, void* stream) {
+  if (!workspace || !nll_sum) return zf::einval("NULL argument");
+  if (N <= 0) {
+    ZF_TRY_HIP(hipMemsetAsync(nll_sum, 0, sizeof(double), (hipStream_t)stream));
+    return ZF_OK;
+  }
+  const long long blocks = (N + zf::kBlockRows - 1) / zf::kBlockRows;
+  hipLaunchKernelGGL(zf::reduce_partials, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)workspace, blocks, nll_sum);
+  ZF_CHECK_LAUNCH("reduce_partials");
+  return ZF_OK;
+}
+
+int zf_flow_log_prob(zf_flow_t* h, const float* x, const float* c, float* log_prob,
+                     double* nll_sum, void* workspace, int64_t N, void* stream) {
+  if (!h) return zf::einval("handle is NULL");
+  return zf_flow_log_prob_segment(h, 0, h->host.n_ops, x, c, nullptr, log_prob, nll_sum,
+                                  workspace, N, stream);
+}
+
+int zf_flow_forward(zf_flow_t* h, int op_begin, int op_end, const float* x, const float* c,
+                    float* y, const float* log_det_in, float* log_det, int64_t N, void* stream) {
+  return zf::launch_flow<false>(h, op_begin, op_end, x, c, y, log_det_in, log_det, nullptr,
+                                nullptr, N, stream);
+}
+
+int zf_flow_inverse(zf_flow_t* h, int op_begin, int op_end, const float* z, const float* c,
+                    float* x, int64_t N, void* stream) {
+  if (!x && N > 0) return zf::einval("x is NULL");
+  return zf::launch_flow<true>(h, op_begin, op_end, z, c, x, nullptr, nullptr, nullptr, nullptr,
+                               N, stream);
+}
+
+static int upload_region(zf_flow* h, int64_t off, int64_t n) {
+  ZF_TRY_HIP(hipSetDevice(h->device));
+  ZF_TRY_HIP(hipDeviceSynchronize());  // no kernel may still read the blob
+  ZF_TRY_HIP(hipMemcpy(h->d_blob + off, h->packed.data() + off, n * sizeof(float),
+                       hipMemcpyHostToDevice));
+  return ZF_OK;
+}
+
+int zf_flow_set_bn_stats(zf_flow_t* h, int op, const float* mean, const float* var) {
+  if (!h || !mean || !var) return zf::einval("NULL argument");
+  if (op < 0 || op >= h->desc.n_ops || h->desc.ops[op].kind != ZF_OP_NSC) return zf::einval("op %d is not an NSC", op);
+  const zf_op_desc& od = h->desc.ops[op];
+  const zf::OpGeom g = zf::nsc_geom(&h->desc, od);
+  float* nat = h->natural.data() + od.off_bn;
+  for (int k = 0; k < g.DC; ++k) { nat[k] = mean[k]; nat[g.DC + k] = var[k]; }
+  zf::pack_nsc_bn(&h->desc, od, h->natural.data(), h->packed.data() + h->host.ops[op].bn);
+  return upload_region(h, h->host.ops[op].bn, 3 * 2 * g.KS0);
+}
+
+int zf_flow_set_sb_stats(zf_flow_t* h, int op, const float* xmin, const float* xmax) {
+  if (!h || !xmin || !xmax) return zf::einval("NULL argument");
+  if (op < 0 || op >= h->desc.n_ops || h->desc.ops[op].kind != ZF_OP_SHIFT_BOUNDS) return zf::einval("op %d is not a ShiftBounds", op);
+  const zf_op_desc& od = h->desc.ops[op];
+  for (int i = 0; i < h->desc.dim; ++i) {
+    h->natural[od.off_sb + 8 * i + 3] = xmin[i];
+    h->natural[od.off_sb + 8 * i + 4] = xmax[i];
+  }
+  zf::pack_sb(&h->desc, od, h->natural.data(), h->packed.data() + h->host.ops[op].sb);
+  return upload_region(h, h->host.ops[op].sb, 8 * h->desc.dim);
+}
+
+}  // extern "C"

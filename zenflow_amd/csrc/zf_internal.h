@@ -1,0 +1,47 @@
+// Internal helpers shared by the libzenflow_amd translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/zenflow_amd.h"
+
+namespace zf {
+
+void set_error(const char* fmt, ...);
+
+// Returns 0 or the (positive) hipError_t, recording a message.
+inline int hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return ZF_OK;
+  set_error("%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+  return (int)e;
+}
+
+inline int einval(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  set_error("%s", buf);
+  return ZF_EINVAL;
+}
+
+inline int enotsup(const char* msg) {
+  set_error("not supported: %s", msg);
+  return ZF_ENOTSUP;
+}
+
+#define ZF_TRY_HIP(expr)                                   \
+  do {                                                     \
+    int _zf_rc = ::zf::hip_status((expr), #expr);          \
+    if (_zf_rc != ZF_OK) return _zf_rc;                    \
+  } while (0)
+
+// Post-launch check: a bad launch configuration surfaces here.
+#define ZF_CHECK_LAUNCH(name) ZF_TRY_HIP(hipGetLastError())
+
+}  // namespace zf

@@ -1,0 +1,218 @@
+// K1 — standalone rational-quadratic spline kernels at the `zenflow.utils`
+// boundary (utils.rational_quadratic_spline_forward/inverse, utils.py:65-202;
+// normalize_spline_params, utils.py:37-62).
+//
+// HBM-bound: per (row, dim) item the kernel reads x + dx[K] + dy[K] + slope[K-1]
+// and writes y (+ one log_det per row): 4*(3K+1) bytes per item + 4 per row.
+// A block stages R whole rows (R*N items) of parameters HBM -> LDS with
+// coalesced dwordx4 loads (row stride K+1 in LDS: conflict-free per-item
+// reads), then one thread per item runs the bin search + spline in registers;
+// the row log-det is summed in dim order (utils.py:139) through LDS.
+#include "zf_internal.h"
+#include "zf_spline.h"
+
+namespace zf {
+namespace {
+
+constexpr int kK1Threads = 256;
+constexpr int kK1LdsBudgetFloats = 12288;  // 48 KiB per block
+
+struct LdsParams {
+  const float* dx;  // item stride K+1
+  const float* dy;
+  const float* sl;  // item stride K+1 (K-1 used)
+  int ks;
+  __device__ float w(int j) const { return dx[j]; }
+  __device__ float h(int j) const { return dy[j]; }
+  __device__ float d(int j) const { return sl[j]; }
+};
+
+// Copy `n` contiguous floats src[0..n) into LDS rows of `K` values with stride
+// `ks` (dst[(f/K)*ks + f%K]).  dwordx4 loads where the source is 16-B aligned.
+__device__ __forceinline__ void stage_rows(float* dst, const float* __restrict__ src, int64_t n,
+                                           int K, int ks) {
+  const int tid = threadIdx.x;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
+  int64_t head = 0;
+  if (addr & 15) head = (16 - (addr & 15)) / 4;
+  if (head > n) head = n;
+  for (int64_t f = tid; f < head; f += blockDim.x) {
+    const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
+    dst[it * ks + j] = src[f];
+  }
+  const int64_t nv = (n - head) / 4;
+  const float4* src4 = reinterpret_cast<const float4*>(src + head);
+  for (int64_t q = tid; q < nv; q += blockDim.x) {
+    const float4 v = src4[q];
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t f = head + 4 * q + e;
+      const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
+      dst[it * ks + j] = vv[e];
+    }
+  }
+  for (int64_t f = head + 4 * nv + tid; f < n; f += blockDim.x) {
+    const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
+    dst[it * ks + j] = src[f];
+  }
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(kK1Threads) void rqs_kernel(
+    const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
+    const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
+    int64_t M, int N, int K, int R) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int ks = (K % 2 == 0) ? K + 1 : K + 2;  // odd LDS row stride: conflict-free
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  if (r0 >= M) return;
+  const int rows = (int)((M - r0) < R ? (M - r0) : R);
+  const int items = rows * N;
+  const int64_t item0 = r0 * N;
+  float* s_dx = lds;
+  float* s_dy = s_dx + (size_t)R * N * ks;
+  float* s_sl = s_dy + (size_t)R * N * ks;
+  float* s_ld = s_sl + (size_t)R * N * ks;
+
+  stage_rows(s_dx, dx + item0 * K, (int64_t)items * K, K, ks);
+  stage_rows(s_dy, dy + item0 * K, (int64_t)items * K, K, ks);
+  if (K > 1) stage_rows(s_sl, slope + item0 * (K - 1), (int64_t)items * (K - 1), K - 1, ks);
+  __syncthreads();
+
+  const int i = threadIdx.x;
+  if (i < items) {
+    const float v = xin[item0 + i];
+    LdsParams p{s_dx + i * ks, s_dy + i * ks, s_sl + i * ks, ks};
+    const RqsBin b = rqs_bin<FWD>(v, K, p);
+    if (FWD) {
+      float y, ld;
+      rqs_forward_eval(v, b, y, ld);
+      if (out) out[item0 + i] = y;
+      s_ld[i] = ld;
+    } else {
+      out[item0 + i] = rqs_inverse_eval(v, b);
+    }
+  }
+  if (FWD && log_det) {
+    __syncthreads();
+    if (i < rows) {
+      float acc = 0.f;  // log_det.sum(axis=1), dim order
+      for (int n = 0; n < N; ++n) acc = acc + s_ld[i * N + n];
+      log_det[r0 + i] = acc;
+    }
+  }
+}
+
+// utils.py:23-34, 37-62 — one thread per row.
+__global__ void normalize_kernel(float* __restrict__ dx, float* __restrict__ dy,
+                                 float* __restrict__ sl, int64_t M, int K) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // Python floats (utils.py:32)
+  const float c = (float)c64;
+  const float norm = (float)(1.0 + c64 * (double)K);
+  float* rows[2] = {dx + m * K, dy + m * K};
+  for (int a = 0; a < 2; ++a) {
+    float* r = rows[a];
+    float xs = 0.f;
+    for (int j = 0; j < K; ++j) { const float s = squareplus(r[j]); r[j] = s; xs = xs + s; }
+    for (int j = 0; j < K; ++j) r[j] = (r[j] / xs + c) / norm;
+  }
+  float* s = sl + m * (K - 1);
+  for (int j = 0; j < K - 1; ++j) s[j] = squareplus(s[j]);
+}
+
+// utils.py:18-20 elementwise; b is the reference's `b` argument.
+__global__ void squareplus_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                  float b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { const float v = x[i]; y[i] = 0.5f * (v + __builtin_sqrtf(v * v + b)); }
+}
+
+// utils.py:23-34 over rows of K; c and 1 + c*n are float64 Python scalars.
+__global__ void softmax_threshold_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                         int64_t M, int K, float c, float norm) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float* r = x + m * K;
+  float* o = y + m * K;
+  float xs = 0.f;
+  for (int j = 0; j < K; ++j) xs = xs + squareplus(r[j]);
+  for (int j = 0; j < K; ++j) o[j] = (squareplus(r[j]) / xs + c) / norm;
+}
+
+template <bool FWD>
+int launch_rqs(const float* x, const float* dx, const float* dy, const float* slope, float* out,
+               float* log_det, int64_t M, int N, int K, void* stream) {
+  if (M < 0 || N <= 0 || K < 1 || K > 256) return einval("bad shape M=%lld N=%d K=%d", (long long)M, N, K);
+  if (M == 0) return ZF_OK;
+  if (!x || !dx || !dy || (K > 1 && !slope)) return einval("NULL input");
+  if (!FWD && !out) return einval("NULL output");
+  const int ks = (K % 2 == 0) ? K + 1 : K + 2;
+  const int per_item = 3 * ks + 1;
+  int R = kK1LdsBudgetFloats / (per_item * N);
+  if (R > kK1Threads / N) R = kK1Threads / N;
+  if (R < 1) return enotsup("N*(3K+4) too large for one block (N > 256 or K too large)");
+  const size_t lds = sizeof(float) * (size_t)R * N * per_item;
+  const int64_t grid = (M + R - 1) / R;
+  if (grid > 0x7fffffffLL) return einval("M too large");
+  hipLaunchKernelGGL(rqs_kernel<FWD>, dim3((unsigned)grid), dim3(kK1Threads), lds,
+                     (hipStream_t)stream, x, dx, dy, slope, out, log_det, M, N, K, R);
+  ZF_CHECK_LAUNCH("rqs_kernel");
+  return ZF_OK;
+}
+
+}  // namespace
+}  // namespace zf
+
+extern "C" {
+
+int zf_rqs_forward(const float* x, const float* dx, const float* dy, const float* slope,
+                   float* y, float* log_det, int64_t M, int N, int K, void* stream) {
+  return zf::launch_rqs<true>(x, dx, dy, slope, y, log_det, M, N, K, stream);
+}
+
+int zf_rqs_inverse(const float* y, const float* dx, const float* dy, const float* slope,
+                   float* x, int64_t M, int N, int K, void* stream) {
+  return zf::launch_rqs<false>(y, dx, dy, slope, x, nullptr, M, N, K, stream);
+}
+
+int zf_squareplus(const float* x, float* y, int64_t n, float b, void* stream) {
+  if (n < 0) return zf::einval("n < 0");
+  if (n == 0) return ZF_OK;
+  if (!x || !y) return zf::einval("NULL argument");
+  const int64_t grid = (n + 255) / 256;
+  hipLaunchKernelGGL(zf::squareplus_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     x, y, n, b);
+  ZF_CHECK_LAUNCH("squareplus_kernel");
+  return ZF_OK;
+}
+
+int zf_softmax_with_threshold(const float* x, float* y, int64_t M, int K, double threshold,
+                              void* stream) {
+  if (M < 0 || K < 1) return zf::einval("bad shape");
+  if (M == 0) return ZF_OK;
+  if (!x || !y) return zf::einval("NULL argument");
+  const double c64 = threshold / (1.0 - (double)K * threshold);
+  const int64_t grid = (M + 255) / 256;
+  hipLaunchKernelGGL(zf::softmax_threshold_kernel, dim3((unsigned)grid), dim3(256), 0,
+                     (hipStream_t)stream, x, y, M, K, (float)c64, (float)(1.0 + c64 * (double)K));
+  ZF_CHECK_LAUNCH("softmax_threshold_kernel");
+  return ZF_OK;
+}
+
+int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, int K,
+                               void* stream) {
+  if (M < 0 || K < 1) return zf::einval("bad shape");
+  if (M == 0) return ZF_OK;
+  if (!dx || !dy || (K > 1 && !slope)) return zf::einval("NULL input");
+  const int threads = 256;
+  const int64_t grid = (M + threads - 1) / threads;
+  hipLaunchKernelGGL(zf::normalize_kernel, dim3((unsigned)grid), dim3(threads), 0,
+                     (hipStream_t)stream, dx, dy, slope, M, K);
+  ZF_CHECK_LAUNCH("normalize_kernel");
+  return ZF_OK;
+}
+
+}  // extern "C"

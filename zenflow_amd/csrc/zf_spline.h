@@ -1,0 +1,95 @@
+// Rational-quadratic spline device math (Durkan et al. 2019), restating the
+// reference semantics of src/zenflow/utils.py:65-250 exactly, including its
+// numerically "impure" details (EPS inside logs/denominators, z clip, the
+// out-of-bounds identity, the fill-mode gather at the idx == K sliver).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace zf {
+
+constexpr float kEps = 1e-5f;            // utils.py:15
+constexpr float kOneMinusEps = 0.99999f; // 1 - EPS, a Python float rounded to fp32 (utils.py:123)
+
+__device__ __forceinline__ float qnan() { return __builtin_nanf(""); }
+
+// utils.py:18-20  squareplus(x, b=4) = 0.5 * (x + sqrt(x^2 + b))
+__device__ __forceinline__ float squareplus(float x) {
+  return 0.5f * (x + __builtin_sqrtf(x * x + 4.0f));
+}
+
+// Bin parameters gathered at idx (utils.py:205-232 `_compute_rqs_input`).
+struct RqsBin {
+  float xk, yk, w, h, dk, dkp1, sk;
+  bool oob;
+};
+
+// Bin search + gather (utils.py:220-232, `_index` :244-250, `_knots` :235-241).
+//   P provides  w(j) = dx_j, h(j) = dy_j (0 <= j < K), d(j) = slope_j (0 <= j < K-1).
+// Count semantics of `_index`: idx = clip(#{k : knot_k <= v} - 1, 0, K), with
+// knots = [0, cumsum]. For the (usual) monotone knots this is the last bin
+// whose left knot is <= v; a non-monotone parameter set (never produced by
+// normalize_spline_params) falls back to re-summing the knots up to idx.
+// jnp.take_along_axis defaults to mode="fill": an out-of-range gather gives NaN
+// (idx == K => dx, dy, sk, dk[idx+1] are NaN).
+template <bool FWD, class P>
+__device__ __forceinline__ RqsBin rqs_bin(float v, int K, const P& p) {
+  float xk = 0.f, yk = 0.f;
+  float sxk = 0.f, syk = 0.f;
+  int cnt = 0, sel = 0;
+  for (int j = 0; j < K; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = j; sxk = xk; syk = yk; }
+    xk = xk + p.w(j);
+    yk = yk + p.h(j);
+  }
+  {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; }
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  if (idx != sel) {  // non-monotone knots: reproduce the gather at idx exactly
+    xk = 0.f; yk = 0.f;
+    for (int j = 0; j < idx; ++j) { xk = xk + p.w(j); yk = yk + p.h(j); }
+    sxk = xk; syk = yk; sel = idx;
+  }
+  RqsBin b;
+  b.xk = sxk;
+  b.yk = syk;
+  b.w = sel < K ? p.w(sel) : qnan();
+  b.h = sel < K ? p.h(sel) : qnan();
+  b.dk = (sel == 0 || sel == K) ? 1.0f : p.d(sel - 1);             // dk = [1, slope, 1]
+  b.dkp1 = (sel + 1 < K) ? p.d(sel) : (sel + 1 == K ? 1.0f : qnan());
+  b.sk = b.h / b.w;                                                 // sk = dy / dx
+  b.oob = (v < 0.f) || (v >= 1.f);                                  // :245
+  return b;
+}
+
+// utils.py:121-139 — forward value and per-dim log|dy/dx|.
+__device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
+  const float zr = (x - b.xk) / b.w;               // :122
+  // :123 jnp.clip propagates NaN (fmaxf/fminf would drop it)
+  const float z = (zr != zr) ? zr : fminf(fmaxf(zr, kEps), kOneMinusEps);
+  const float az = 1.0f - z;
+  const float num = b.h * z * (b.sk * z + b.dk * az);              // :125
+  const float den = b.sk + (b.dkp1 + b.dk - 2.0f * b.sk) * z * az;  // :126
+  const float yv = b.yk + num / (den + kEps);                       // :127
+  y = b.oob ? x : yv;                                               // :130
+  const float num2 = z * (b.dkp1 * z + 2.0f * b.sk * az) + b.dk * (az * az);  // :133
+  const float l = 2.0f * logf(b.sk + kEps) + logf(num2 + kEps) - 2.0f * logf(den + kEps);
+  ld = b.oob ? 0.0f : l;                                            // :138
+}
+
+// utils.py:191-201 — inverse via the quadratic root.
+__device__ __forceinline__ float rqs_inverse_eval(float y, const RqsBin& b) {
+  const float dy = y - b.yk;
+  const float t = b.dkp1 + b.dk - 2.0f * b.sk;
+  const float a = b.h * (b.sk - b.dk) + dy * t;  // :193
+  const float bb = b.h * b.dk - dy * t;          // :194
+  const float c = -b.sk * dy;                    // :195
+  const float z = 2.0f * c / (-bb - __builtin_sqrtf(bb * bb - 4.0f * a * c));  // :197
+  const float x = z * b.w + b.xk;                // :198
+  return b.oob ? y : x;                          // :201
+}
+
+}  // namespace zf
