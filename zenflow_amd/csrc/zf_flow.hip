@@ -62,9 +62,91 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// flax.linen.swish = x * sigmoid(x) = x / (1 + exp(-x)) (bijectors.py:319).
+// exp(-x) = 2^t * (1 + lo*ln2) with t = -x*log2e rounded and lo its exact
+// residual (fma) plus the log2e tail: ~1 ulp instead of the |x|*6e-8 relative
+// error of a bare v_exp_f32(-x*log2e); the reciprocal gets one Newton step.
+#ifndef ZF_SWISH_MODE
+#define ZF_SWISH_MODE 1
+#endif
+#ifndef ZF_KNOT_MODE
+#define ZF_KNOT_MODE 1
+#endif
 __device__ __forceinline__ float swish(float v) {
-  // flax.linen.swish = x * sigmoid(x) (bijectors.py:319)
+#if ZF_SWISH_MODE == 0
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.44269504f));
+#elif ZF_SWISH_MODE == 2
+  return v * (1.0f / (1.0f + expf(-v)));
+#endif
+  constexpr float kL2E = 1.44269502162933349609375f;  // fp32(log2 e)
+  constexpr float kL2ELo = 1.925963033500011e-08f;    // log2 e - kL2E
+  constexpr float kLn2 = 0.693147180559945f;
+  const float nv = -v;
+  const float t = nv * kL2E;
+  const float lo = __builtin_fmaf(nv, kL2E, -t) + nv * kL2ELo;
+  const float p = __builtin_amdgcn_exp2f(t);
+  const float e = (p == INFINITY) ? p : __builtin_fmaf(p, lo * kLn2, p);
+  const float d = 1.0f + e;
+  float r = __builtin_amdgcn_rcpf(d);
+  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+  return v * r;
+}
+
+// 1/x to ~0.5 ulp: hardware reciprocal + one Newton step.
+__device__ __forceinline__ float rcp_refined(float x) {
+  float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+}
+
+// x / d given r = rcp_refined(d): one residual correction of the product
+// makes the quotient correctly rounded for these (normal, non-overflowing)
+// operands — the IEEE division the reference performs, at a third of the cost.
+__device__ __forceinline__ float div_cr(float x, float d, float r) {
+  const float q = x * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
+}
+
+// squareplus (utils.py:18-20) with a residual-corrected hardware square root
+// (x^2 + 4 >= 4: never denormal); matches the correctly rounded sqrtf.
+__device__ __forceinline__ float squareplus_fast(float x) {
+  const float a = x * x + 4.0f;
+  float sq = __builtin_amdgcn_sqrtf(a);
+  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * __builtin_amdgcn_rcpf(sq), sq);
+  return 0.5f * (x + sq);
+}
+
+// One 32-row output tile of a Dense layer on MFMA: acc = W^T[tile] . H over
+// the T input tiles (activations hb: unit rows in registers, sample on the
+// lane).  The weight fragments of one input tile (4 dwordx4 per lane, 16
+// MFMAs) are streamed with exactly one chunk in flight: `cur` holds this
+// tile's first chunk on entry and the next tile's (pnext, may be null) on exit.
+template <int T>
+__device__ __forceinline__ floatx16 mfma_tile(const floatx4* __restrict__ p,
+                                              const floatx4* __restrict__ pnext, floatx4 (&cur)[4],
+                                              const floatx16 (&hb)[T]) {
+  floatx16 acc = floatx16{0};
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    floatx4 nxt[4];
+    const bool more = (t + 1 < T);
+    const floatx4* src = more ? p + (t + 1) * 256 : pnext;
+    const bool have = more || (pnext != nullptr);
+    if (have) {
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) nxt[r4] = src[r4 * 64];
+    }
+    asm volatile("" ::: "memory");  // keep the next chunk's loads here, not hoisted
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[r4][e], hb[t][4 * r4 + e], acc, 0, 0, 0);
+    if (have) {
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) cur[r4] = nxt[r4];
+    }
+  }
+  return acc;
 }
 
 __device__ __forceinline__ int pmod(int a, int m) {
@@ -78,18 +160,31 @@ struct RingParams {
   const float* ring;  // wave ring base + s
   int base;           // d * S
   int K, mask;
-  float sx, sy, c, norm;
+  float sx, sy, rsx, rsy;  // sum(squareplus) and refined reciprocals
+  float c, norm, rnorm;    // threshold c, 1 + c*K and its reciprocal
   __device__ __forceinline__ float at(int q) const {
     return ring[(((q >> 5) & mask) << 10) + ((q & 31) << 5)];
   }
-  // softmax_with_threshold (utils.py:23-34); squareplus values were stored in place
+  // softmax_with_threshold (utils.py:23-34): (x / xs + c) / (1 + c*n), both
+  // divisions correctly rounded (div_cr); squareplus values were stored in place.
+#if ZF_KNOT_MODE == 0
   __device__ __forceinline__ float w(int j) const { return (at(base + j) / sx + c) / norm; }
   __device__ __forceinline__ float h(int j) const { return (at(base + K + j) / sy + c) / norm; }
-  __device__ __forceinline__ float d(int j) const { return squareplus(at(base + 2 * K + j)); }
+#else
+  __device__ __forceinline__ float w(int j) const {
+    return div_cr(div_cr(at(base + j), sx, rsx) + c, norm, rnorm);
+  }
+  __device__ __forceinline__ float h(int j) const {
+    return div_cr(div_cr(at(base + K + j), sy, rsy) + c, norm, rnorm);
+  }
+#endif
+  __device__ __forceinline__ float d(int j) const { return squareplus_fast(at(base + 2 * K + j)); }
 };
 
+// 2 waves per SIMD (<= 256 VGPR+AGPR) up to 4 activation tiles; the 8-tile
+// (hidden 256) variant needs the whole register file.
 template <int HP, bool INV>
-__global__ __launch_bounds__(kWaves * 64) void flow_kernel(
+__global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const float* __restrict__ xin,
     const float* __restrict__ cin, float* __restrict__ y_out, const float* __restrict__ ld_in,
     float* __restrict__ ld_out, float* __restrict__ lp_out, double* __restrict__ block_partial,
@@ -192,24 +287,23 @@ __global__ __launch_bounds__(kWaves * 64) void flow_kernel(
           for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + b0[o * 32 + r]);
       }
       // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.
+      floatx4 wc[4];
       for (int l = 1; l < op.n_hidden; ++l) {
         const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[l]) + lane;
-        const float* bl = blob + op.b[l] + hh * 16;
+        const floatx4* bl4 = reinterpret_cast<const floatx4*>(blob + op.b[l] + hh * 16);
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) wc[r4] = wl[r4 * 64];
         floatx16 ho[T];
 #pragma unroll
         for (int o = 0; o < T; ++o) {
-          floatx16 acc = floatx16{0};
+          const floatx4* nx = (o + 1 < T) ? wl + (o + 1) * T * 256 : nullptr;
+          floatx16 acc = mfma_tile<T>(wl + o * T * 256, nx, wc, hb);
 #pragma unroll
-          for (int t = 0; t < T; ++t)
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const floatx4 bv = bl4[o * 8 + r4];
 #pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-              const floatx4 w = wl[((o * T + t) * 4 + r4) * 64];
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[e], hb[t][4 * r4 + e], acc, 0, 0, 0);
-            }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[r] = swish(acc[r] + bl[o * 32 + r]);
+            for (int e = 0; e < 4; ++e) acc[4 * r4 + e] = swish(acc[4 * r4 + e] + bv[e]);
+          }
           ho[o] = acc;
         }
 #pragma unroll
@@ -223,19 +317,15 @@ __global__ __launch_bounds__(kWaves * 64) void flow_kernel(
       const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
       const float cth = (float)c64;
       const float norm = (float)(1.0 + c64 * (double)K);
+      const float rnorm = rcp_refined(norm);
       int next_d = 0;
       float ldc = 0.f;
-      for (int o = 0; o < op.T_last; ++o) {
-        floatx16 acc = floatx16{0};
+      const int T_last = op.T_last;
 #pragma unroll
-        for (int t = 0; t < T; ++t)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const floatx4 w = wl[((o * T + t) * 4 + r4) * 64];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[e], hb[t][4 * r4 + e], acc, 0, 0, 0);
-          }
+      for (int r4 = 0; r4 < 4; ++r4) wc[r4] = wl[r4 * 64];
+      for (int o = 0; o < T_last; ++o) {
+        const floatx4* nx = (o + 1 < T_last) ? wl + (o + 1) * T * 256 : nullptr;
+        floatx16 acc = mfma_tile<T>(wl + o * T * 256, nx, wc, hb);
         float* slot = ring + ((o & mask) << 10) + s;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -259,13 +349,14 @@ __global__ __launch_bounds__(kWaves * 64) void flow_kernel(
             p.mask = mask;
             p.c = cth;
             p.norm = norm;
+            p.rnorm = rnorm;
             float* rp = ring + s;
             float sx = 0.f, sy = 0.f;
             for (int j = 0; j < K; ++j) {  // squareplus in place + sums (utils.py:30-33)
               const int qx = p.base + j, qy = p.base + K + j;
               float* ax = rp + (((qx >> 5) & mask) << 10) + ((qx & 31) << 5);
               float* ay = rp + (((qy >> 5) & mask) << 10) + ((qy & 31) << 5);
-              const float vx = squareplus(*ax), vy = squareplus(*ay);
+              const float vx = squareplus_fast(*ax), vy = squareplus_fast(*ay);
               *ax = vx;
               *ay = vy;
               sx = sx + vx;
@@ -273,6 +364,8 @@ __global__ __launch_bounds__(kWaves * 64) void flow_kernel(
             }
             p.sx = sx;
             p.sy = sy;
+            p.rsx = rcp_refined(sx);
+            p.rsy = rcp_refined(sy);
             float* xp = xs + pmod(d + rot, D) * 32 + s;
             const float xv = *xp;
             const RqsBin bin = rqs_bin<!INV>(xv, K, p);

@@ -27,10 +27,14 @@ struct LdsParams {
   __device__ float d(int j) const { return sl[j]; }
 };
 
-// Copy `n` contiguous floats src[0..n) into LDS rows of `K` values with stride
-// `ks` (dst[(f/K)*ks + f%K]).  dwordx4 loads where the source is 16-B aligned.
+// Copy `n` contiguous floats src[0..n) into LDS rows of `KX` values with
+// stride `ks` (dst[(f/KX)*ks + f%KX]): dwordx4 loads (coalesced, 16 B/lane)
+// where the source is 16-B aligned.  KX > 0 is a compile-time item width
+// (constant-divisor index split); KX == 0 takes the runtime width `kx`.
+template <int KX>
 __device__ __forceinline__ void stage_rows(float* dst, const float* __restrict__ src, int64_t n,
-                                           int K, int ks) {
+                                           int kx, int ks) {
+  const int K = KX > 0 ? KX : kx;
   const int tid = threadIdx.x;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(src);
   int64_t head = 0;
@@ -40,29 +44,31 @@ __device__ __forceinline__ void stage_rows(float* dst, const float* __restrict__
     const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
     dst[it * ks + j] = src[f];
   }
-  const int64_t nv = (n - head) / 4;
+  const int nv = (int)((n - head) / 4);
   const float4* src4 = reinterpret_cast<const float4*>(src + head);
-  for (int64_t q = tid; q < nv; q += blockDim.x) {
+  const int h = (int)head;
+  for (int q = tid; q < nv; q += blockDim.x) {
     const float4 v = src4[q];
     const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int64_t f = head + 4 * q + e;
-      const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
+      const unsigned f = (unsigned)(h + 4 * q + e);
+      const unsigned it = f / (unsigned)K, j = f - it * (unsigned)K;
       dst[it * ks + j] = vv[e];
     }
   }
-  for (int64_t f = head + 4 * nv + tid; f < n; f += blockDim.x) {
+  for (int64_t f = head + 4 * (int64_t)nv + tid; f < n; f += blockDim.x) {
     const int it = (int)(f / K), j = (int)(f - (int64_t)it * K);
     dst[it * ks + j] = src[f];
   }
 }
 
-template <bool FWD>
+template <bool FWD, int KT>
 __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
     const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
     const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
-    int64_t M, int N, int K, int R) {
+    int64_t M, int N, int Kr, int R) {
+  const int K = KT > 0 ? KT : Kr;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int ks = (K % 2 == 0) ? K + 1 : K + 2;  // odd LDS row stride: conflict-free
   const int64_t r0 = (int64_t)blockIdx.x * R;
@@ -75,9 +81,10 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
   float* s_sl = s_dy + (size_t)R * N * ks;
   float* s_ld = s_sl + (size_t)R * N * ks;
 
-  stage_rows(s_dx, dx + item0 * K, (int64_t)items * K, K, ks);
-  stage_rows(s_dy, dy + item0 * K, (int64_t)items * K, K, ks);
-  if (K > 1) stage_rows(s_sl, slope + item0 * (K - 1), (int64_t)items * (K - 1), K - 1, ks);
+  stage_rows<KT>(s_dx, dx + item0 * K, (int64_t)items * K, K, ks);
+  stage_rows<KT>(s_dy, dy + item0 * K, (int64_t)items * K, K, ks);
+  if (K > 1)
+    stage_rows<(KT > 1 ? KT - 1 : 0)>(s_sl, slope + item0 * (K - 1), (int64_t)items * (K - 1), K - 1, ks);
   __syncthreads();
 
   const int i = threadIdx.x;
@@ -157,8 +164,18 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
   const size_t lds = sizeof(float) * (size_t)R * N * per_item;
   const int64_t grid = (M + R - 1) / R;
   if (grid > 0x7fffffffLL) return einval("M too large");
-  hipLaunchKernelGGL(rqs_kernel<FWD>, dim3((unsigned)grid), dim3(kK1Threads), lds,
-                     (hipStream_t)stream, x, dx, dy, slope, out, log_det, M, N, K, R);
+  hipStream_t st = (hipStream_t)stream;
+#define ZF_RQS(KV)                                                                              \
+  hipLaunchKernelGGL((rqs_kernel<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), lds, st, x, \
+                     dx, dy, slope, out, log_det, M, N, K, R)
+  switch (K) {
+    case 4: ZF_RQS(4); break;
+    case 8: ZF_RQS(8); break;
+    case 16: ZF_RQS(16); break;
+    case 32: ZF_RQS(32); break;
+    default: ZF_RQS(0); break;
+  }
+#undef ZF_RQS
   ZF_CHECK_LAUNCH("rqs_kernel");
   return ZF_OK;
 }
