@@ -80,7 +80,7 @@ def test_normalize_and_squareplus_vs_oracle():
     assert_allclose(u.squareplus(a), O.squareplus(a), rtol=1e-5)
 
 
-@pytest.mark.parametrize("K", [1, 2, 3, 8, 16, 32, 64])
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8, 16, 32, 64])
 @pytest.mark.parametrize("N", [1, 2, 3, 8])
 def test_rqs_parity(K, N):
     """Random normalised params incl. out-of-bounds x; y, log_det and inverse."""

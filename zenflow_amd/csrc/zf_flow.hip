@@ -66,8 +66,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 // exp(-x) = 2^t * (1 + lo*ln2) with t = -x*log2e rounded and lo its exact
 // residual (fma) plus the log2e tail: ~1 ulp instead of the |x|*6e-8 relative
 // error of a bare v_exp_f32(-x*log2e); the reciprocal gets one Newton step.
+// 0: v * rcp(1 + 2^(-v*log2e))  (6 VALU, ~|v|*6e-8 relative error)
+// 1: compensated exp argument + Newton reciprocal (~1 ulp, 16 VALU)
+// 2: expf + IEEE division (reference form)
+// All three give the same mean log_prob error as the fp32 oracle
+// (scripts/diag_parity.py); 0 is the default.
 #ifndef ZF_SWISH_MODE
-#define ZF_SWISH_MODE 1
+#define ZF_SWISH_MODE 0
 #endif
 #ifndef ZF_KNOT_MODE
 #define ZF_KNOT_MODE 1
@@ -162,9 +167,9 @@ struct RingParams {
   int K, mask;
   float sx, sy, rsx, rsy;  // sum(squareplus) and refined reciprocals
   float c, norm, rnorm;    // threshold c, 1 + c*K and its reciprocal
-  __device__ __forceinline__ float at(int q) const {
-    return ring[(((q >> 5) & mask) << 10) + ((q & 31) << 5)];
-  }
+  // row q of the last layer lives at ring slot (q >> 5) & (nslot-1), row q & 31:
+  // ((q>>5)&mask)*1024 + (q&31)*32 == (q & (32*nslot-1)) * 32
+  __device__ __forceinline__ float at(int q) const { return ring[(q & mask) << 5]; }
   // softmax_with_threshold (utils.py:23-34): (x / xs + c) / (1 + c*n), both
   // divisions correctly rounded (div_cr); squareplus values were stored in place.
 #if ZF_KNOT_MODE == 0
@@ -346,7 +351,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
             p.ring = ring + s;
             p.base = d * S;
             p.K = K;
-            p.mask = mask;
+            p.mask = (mask << 5) | 31;
             p.c = cth;
             p.norm = norm;
             p.rnorm = rnorm;
@@ -354,8 +359,8 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
             float sx = 0.f, sy = 0.f;
             for (int j = 0; j < K; ++j) {  // squareplus in place + sums (utils.py:30-33)
               const int qx = p.base + j, qy = p.base + K + j;
-              float* ax = rp + (((qx >> 5) & mask) << 10) + ((qx & 31) << 5);
-              float* ay = rp + (((qy >> 5) & mask) << 10) + ((qy & 31) << 5);
+              float* ax = rp + ((qx & p.mask) << 5);
+              float* ay = rp + ((qy & p.mask) << 5);
               const float vx = squareplus_fast(*ax), vy = squareplus_fast(*ay);
               *ax = vx;
               *ay = vy;

@@ -111,6 +111,121 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
   }
 }
 
+// Fast path for K % 4 == 0 (K = 4, 8, 16, 32): dx/dy rows staged with
+// dwordx4 loads -> ds_write_b128 into rows of KP = K+4 floats (80 B at K=16:
+// the 16 lanes of a ds_read_b128 group hit 16 distinct 4-bank slots), read
+// back as K/4 ds_read_b128 into registers; slopes staged with ds_write_b32
+// (odd stride) and only the two the bin needs are read.
+template <int K>
+struct RegParams {
+  const float (&w_)[K];
+  const float (&h_)[K];
+  const float* sl;
+};
+
+template <bool FWD, int K>
+__device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], const float (&h)[K],
+                                               const float* sl) {
+  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  int cnt = 0, sel = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = j; sxk = xk; syk = yk; sw = w[j]; sh = h[j]; }
+    xk = xk + w[j];
+    yk = yk + h[j];
+  }
+  {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; sw = qnan(); sh = qnan(); }
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  if (idx != sel) {  // non-monotone knots (never from normalize_spline_params)
+    xk = 0.f; yk = 0.f;
+    sw = qnan(); sh = qnan();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j == idx) { sw = w[j]; sh = h[j]; }
+      if (j < idx) { xk = xk + w[j]; yk = yk + h[j]; }
+    }
+    sxk = xk; syk = yk; sel = idx;
+  }
+  RqsBin b;
+  b.xk = sxk;
+  b.yk = syk;
+  b.w = sw;
+  b.h = sh;
+  b.dk = (sel == 0 || sel == K) ? 1.0f : sl[sel - 1];
+  b.dkp1 = (sel + 1 < K) ? sl[sel] : (sel + 1 == K ? 1.0f : qnan());
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+
+template <bool FWD, int K>
+__global__ __launch_bounds__(kK1Threads) void rqs_kernel_v4(
+    const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
+    const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
+    int64_t M, int N, int R) {
+  constexpr int KP = K + 4;
+  constexpr int KS = (K % 2 == 0) ? K + 1 : K + 2;
+  constexpr int Q = K / 4;  // dwordx4 per item row
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  if (r0 >= M) return;
+  const int rows = (int)((M - r0) < R ? (M - r0) : R);
+  const int items = rows * N;
+  const int cap = R * N;
+  const int64_t item0 = r0 * N;
+  float* s_dx = lds;
+  float* s_dy = s_dx + (size_t)cap * KP;
+  float* s_sl = s_dy + (size_t)cap * KP;
+  float* s_ld = s_sl + (size_t)cap * KS;
+  const float4* dx4 = reinterpret_cast<const float4*>(dx + item0 * K);
+  const float4* dy4 = reinterpret_cast<const float4*>(dy + item0 * K);
+  const int nq = items * Q;
+  for (int q = threadIdx.x; q < nq; q += kK1Threads) {
+    const int it = q / Q, c = q - it * Q;
+    const float4 a = dx4[q];
+    const float4 b = dy4[q];
+    *reinterpret_cast<float4*>(s_dx + it * KP + 4 * c) = a;
+    *reinterpret_cast<float4*>(s_dy + it * KP + 4 * c) = b;
+  }
+  if (K > 1) stage_rows<K - 1>(s_sl, slope + item0 * (K - 1), (int64_t)items * (K - 1), K - 1, KS);
+  __syncthreads();
+
+  const int i = threadIdx.x;
+  if (i < items) {
+    const float v = xin[item0 + i];
+    float w[K], h[K];
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+      const float4 a = *reinterpret_cast<const float4*>(s_dx + i * KP + 4 * c);
+      const float4 b = *reinterpret_cast<const float4*>(s_dy + i * KP + 4 * c);
+      w[4 * c] = a.x; w[4 * c + 1] = a.y; w[4 * c + 2] = a.z; w[4 * c + 3] = a.w;
+      h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
+    }
+    const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, s_sl + i * KS);
+    if (FWD) {
+      float y, l;
+      rqs_forward_eval(v, bn, y, l);
+      if (out) out[item0 + i] = y;
+      s_ld[i] = l;
+    } else {
+      out[item0 + i] = rqs_inverse_eval(v, bn);
+    }
+  }
+  if (FWD && log_det) {
+    __syncthreads();
+    if (i < rows) {
+      float acc = 0.f;
+      for (int n = 0; n < N; ++n) acc = acc + s_ld[i * N + n];
+      log_det[r0 + i] = acc;
+    }
+  }
+}
+
 // utils.py:23-34, 37-62 — one thread per row.
 __global__ void normalize_kernel(float* __restrict__ dx, float* __restrict__ dy,
                                  float* __restrict__ sl, int64_t M, int K) {
@@ -156,6 +271,31 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
   if (M == 0) return ZF_OK;
   if (!x || !dx || !dy || (K > 1 && !slope)) return einval("NULL input");
   if (!FWD && !out) return einval("NULL output");
+  hipStream_t st = (hipStream_t)stream;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
+  if (aligned && (K == 4 || K == 8 || K == 16 || K == 32)) {
+    const int kp = K + 4, ksl = K + 1;
+    const int per_item = 2 * kp + ksl + 1;
+    int R = kK1LdsBudgetFloats / (per_item * N);
+    if (R > kK1Threads / N) R = kK1Threads / N;
+    if (R >= 1) {
+      const size_t lds = sizeof(float) * (size_t)R * N * per_item;
+      const int64_t grid = (M + R - 1) / R;
+      if (grid > 0x7fffffffLL) return einval("M too large");
+#define ZF_RQS4(KV)                                                                                 \
+  hipLaunchKernelGGL((rqs_kernel_v4<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), lds, st, x, \
+                     dx, dy, slope, out, log_det, M, N, R)
+      switch (K) {
+        case 4: ZF_RQS4(4); break;
+        case 8: ZF_RQS4(8); break;
+        case 16: ZF_RQS4(16); break;
+        default: ZF_RQS4(32); break;
+      }
+#undef ZF_RQS4
+      ZF_CHECK_LAUNCH("rqs_kernel_v4");
+      return ZF_OK;
+    }
+  }
   const int ks = (K % 2 == 0) ? K + 1 : K + 2;
   const int per_item = 3 * ks + 1;
   int R = kK1LdsBudgetFloats / (per_item * N);
@@ -164,7 +304,6 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
   const size_t lds = sizeof(float) * (size_t)R * N * per_item;
   const int64_t grid = (M + R - 1) / R;
   if (grid > 0x7fffffffLL) return einval("M too large");
-  hipStream_t st = (hipStream_t)stream;
 #define ZF_RQS(KV)                                                                              \
   hipLaunchKernelGGL((rqs_kernel<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), lds, st, x, \
                      dx, dy, slope, out, log_det, M, N, K, R)
