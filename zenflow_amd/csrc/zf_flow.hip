@@ -46,6 +46,7 @@ struct DevOp {
   long long b[17];
   long long bn;
   long long sb;
+  long long first_chunk;   // blob offset of this NSC's first streamed weight chunk
 };
 
 struct DevFlow {
@@ -73,9 +74,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 // (scripts/diag_parity.py); 0 is the default.
 #ifndef ZF_SWISH_MODE
 #define ZF_SWISH_MODE 0
-#endif
-#ifndef ZF_KNOT_MODE
-#define ZF_KNOT_MODE 1
 #endif
 __device__ __forceinline__ float swish(float v) {
 #if ZF_SWISH_MODE == 0
@@ -120,6 +118,16 @@ __device__ __forceinline__ float squareplus_fast(float x) {
   return 0.5f * (x + sq);
 }
 
+// Bias of one 32-row output tile for this lane's 16 accumulator rows (packed
+// [2 lane halves][16]).  Callers issue it BEFORE the tile's weight stream:
+// vmcnt retires in order, so a bias load issued after the prefetch of the
+// next weight chunk would make its consumer drain that prefetch too.
+__device__ __forceinline__ void bias_tile(const float* __restrict__ bt, int hh, floatx4 (&b)[4]) {
+  const floatx4* p = reinterpret_cast<const floatx4*>(bt + hh * 16);
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) b[r4] = p[r4];
+}
+
 // One 32-row output tile of a Dense layer on MFMA: acc = W^T[tile] . H over
 // the T input tiles (activations hb: unit rows in registers, sample on the
 // lane).  The weight fragments of one input tile (4 dwordx4 per lane, 16
@@ -138,7 +146,9 @@ __device__ __forceinline__ floatx16 mfma_tile(const floatx4* __restrict__ p,
     const bool have = more || (pnext != nullptr);
     if (have) {
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) nxt[r4] = src[r4 * 64];
+      for (int r4 = 0; r4 < 4; ++r4) {
+        nxt[r4] = src[r4 * 64];
+      }
     }
     asm volatile("" ::: "memory");  // keep the next chunk's loads here, not hoisted
 #pragma unroll
@@ -172,19 +182,71 @@ struct RingParams {
   __device__ __forceinline__ float at(int q) const { return ring[(q & mask) << 5]; }
   // softmax_with_threshold (utils.py:23-34): (x / xs + c) / (1 + c*n), both
   // divisions correctly rounded (div_cr); squareplus values were stored in place.
-#if ZF_KNOT_MODE == 0
-  __device__ __forceinline__ float w(int j) const { return (at(base + j) / sx + c) / norm; }
-  __device__ __forceinline__ float h(int j) const { return (at(base + K + j) / sy + c) / norm; }
-#else
   __device__ __forceinline__ float w(int j) const {
     return div_cr(div_cr(at(base + j), sx, rsx) + c, norm, rnorm);
   }
   __device__ __forceinline__ float h(int j) const {
     return div_cr(div_cr(at(base + K + j), sy, rsy) + c, norm, rnorm);
   }
-#endif
   __device__ __forceinline__ float d(int j) const { return squareplus_fast(at(base + 2 * K + j)); }
 };
+
+// One pair of transformed dims (next_d, next_d+1; lanes 0-31 / 32-63) of the
+// coupling: normalize_spline_params on the raw conditioner rows in the ring
+// (utils.py:37-62), bin search + gather + RQ spline (utils.py:65-250) on the
+// state column, per-dim log-det combined in dim order (utils.py:139).
+template <bool INV>
+__device__ __forceinline__ void spline_pair(float* ring, float* xs, int s, int hh, int next_d, int end,
+                                            int S, int K, int mask, float cth, float norm, float rnorm,
+                                            int rot, int D, float& ldc) {
+  const int d = next_d + hh;
+  float ldv = 0.f;
+  if (d < end) {
+    RingParams p;
+    p.ring = ring + s;
+    p.base = d * S;
+    p.K = K;
+    p.mask = (mask << 5) | 31;
+    p.c = cth;
+    p.norm = norm;
+    p.rnorm = rnorm;
+    float* rp = ring + s;
+    float sx = 0.f, sy = 0.f;
+    for (int j = 0; j < K; ++j) {  // squareplus in place + sums (utils.py:30-33)
+      const int qx = p.base + j, qy = p.base + K + j;
+      float* ax = rp + ((qx & p.mask) << 5);
+      float* ay = rp + ((qy & p.mask) << 5);
+      const float vx = squareplus_fast(*ax), vy = squareplus_fast(*ay);
+      *ax = vx;
+      *ay = vy;
+      sx = sx + vx;
+      sy = sy + vy;
+    }
+    p.sx = sx;
+    p.sy = sy;
+    p.rsx = rcp_refined(sx);
+    p.rsy = rcp_refined(sy);
+    float* xp = xs + pmod(d + rot, D) * 32 + s;
+    const float xv = *xp;
+    const RqsBin bin = rqs_bin<!INV>(xv, K, p);
+    if (!INV) {
+      float yv, l;
+      rqs_forward_eval(xv, bin, yv, l);
+      *xp = yv;
+      ldv = l;
+    } else {
+      *xp = rqs_inverse_eval(xv, bin);
+    }
+  }
+  wave_lds_sync();
+  if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139)
+    const float other = __shfl_xor(ldv, 32);
+    const float first = hh == 0 ? ldv : other;
+    const float second = hh == 0 ? other : ldv;
+    ldc = ldc + first;
+    if (end - next_d == 2) ldc = ldc + second;
+  }
+}
 
 // 2 waves per SIMD (<= 256 VGPR+AGPR) up to 4 activation tiles; the 8-tile
 // (hidden 256) variant needs the whole register file.
@@ -214,6 +276,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
   int rot = 0;  // logical dim j is stored in column (j + rot) mod D
   wave_lds_sync();
 
+  floatx4 wc[4];  // streamed weight chunk
   const int nq = op_end - op_begin;
   for (int q = 0; q < nq; ++q) {
     const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
@@ -269,6 +332,11 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
       const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
       const int DCp = 2 * KS0;
       const float* bn = blob + op.bn;
+      {  // first streamed chunk flies while layer 0 runs
+        const floatx4* f = reinterpret_cast<const floatx4*>(blob + op.first_chunk) + lane;
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) wc[r4] = f[r4 * 64];
+      }
       floatx16 hb[T];
 #pragma unroll
       for (int o = 0; o < T; ++o) hb[o] = floatx16{0};
@@ -284,31 +352,27 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
         for (int o = 0; o < T; ++o)
           hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
       }
-      {
-        const float* b0 = blob + op.b[0] + hh * 16;
 #pragma unroll
-        for (int o = 0; o < T; ++o)
+      for (int o = 0; o < T; ++o) {
+        floatx4 bv[4];
+        bias_tile(blob + op.b[0] + o * 32, hh, bv);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + b0[o * 32 + r]);
+        for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + bv[r >> 2][r & 3]);
       }
-      // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.
-      floatx4 wc[4];
+      // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.  The last
+      // tile of each layer prefetches the next layer's first chunk.
       for (int l = 1; l < op.n_hidden; ++l) {
         const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[l]) + lane;
-        const floatx4* bl4 = reinterpret_cast<const floatx4*>(blob + op.b[l] + hh * 16);
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) wc[r4] = wl[r4 * 64];
+        const floatx4* wnext = reinterpret_cast<const floatx4*>(blob + op.w[l + 1]) + lane;
         floatx16 ho[T];
 #pragma unroll
         for (int o = 0; o < T; ++o) {
-          const floatx4* nx = (o + 1 < T) ? wl + (o + 1) * T * 256 : nullptr;
+          const floatx4* nx = (o + 1 < T) ? wl + (o + 1) * T * 256 : wnext;
+          floatx4 bv[4];
+          bias_tile(blob + op.b[l] + o * 32, hh, bv);
           floatx16 acc = mfma_tile<T>(wl + o * T * 256, nx, wc, hb);
 #pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const floatx4 bv = bl4[o * 8 + r4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[4 * r4 + e] = swish(acc[4 * r4 + e] + bv[e]);
-          }
+          for (int r = 0; r < 16; ++r) acc[r] = swish(acc[r] + bv[r >> 2][r & 3]);
           ho[o] = acc;
         }
 #pragma unroll
@@ -317,7 +381,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
       // Last Dense (:346) -> (N, dt, 3K-1) params (:347), tile by tile through the ring.
       const int K = op.K, S = op.S, mask = op.nslot_mask;
       const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[op.n_hidden]) + lane;
-      const float* bl = blob + op.b[op.n_hidden] + hh * 16;
+      const float* bl = blob + op.b[op.n_hidden];
       // utils.py:32-34: c and 1 + c*n are Python floats (fp64), rounded to fp32 on use
       const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
       const float cth = (float)c64;
@@ -326,73 +390,34 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
       int next_d = 0;
       float ldc = 0.f;
       const int T_last = op.T_last;
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) wc[r4] = wl[r4 * 64];
       for (int o = 0; o < T_last; ++o) {
         const floatx4* nx = (o + 1 < T_last) ? wl + (o + 1) * T * 256 : nullptr;
+        floatx4 bv[4];
+        bias_tile(bl + o * 32, hh, bv);
         floatx16 acc = mfma_tile<T>(wl + o * T * 256, nx, wc, hb);
         float* slot = ring + ((o & mask) << 10) + s;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rr = (r & 3) + 8 * (r >> 2) + 4 * hh;
-          slot[rr * 32] = acc[r] + bl[o * 32 + r];
+          slot[rr * 32] = acc[r] + bv[r >> 2][r & 3];
         }
         wave_lds_sync();
-        // Run the spline for the next pair of transformed dims once all of
-        // their 2*S parameter rows are in the ring: lanes 0-31 take dim
-        // next_d, lanes 32-63 dim next_d+1.
-        while (next_d < dt) {
-          const int end = (next_d + 2 < dt) ? next_d + 2 : dt;
-          if (end * S > (o + 1) * 32) break;
-          const int d = next_d + hh;
-          float ldv = 0.f;
-          if (d < end) {
-            RingParams p;
-            p.ring = ring + s;
-            p.base = d * S;
-            p.K = K;
-            p.mask = (mask << 5) | 31;
-            p.c = cth;
-            p.norm = norm;
-            p.rnorm = rnorm;
-            float* rp = ring + s;
-            float sx = 0.f, sy = 0.f;
-            for (int j = 0; j < K; ++j) {  // squareplus in place + sums (utils.py:30-33)
-              const int qx = p.base + j, qy = p.base + K + j;
-              float* ax = rp + ((qx & p.mask) << 5);
-              float* ay = rp + ((qy & p.mask) << 5);
-              const float vx = squareplus_fast(*ax), vy = squareplus_fast(*ay);
-              *ax = vx;
-              *ay = vy;
-              sx = sx + vx;
-              sy = sy + vy;
-            }
-            p.sx = sx;
-            p.sy = sy;
-            p.rsx = rcp_refined(sx);
-            p.rsy = rcp_refined(sy);
-            float* xp = xs + pmod(d + rot, D) * 32 + s;
-            const float xv = *xp;
-            const RqsBin bin = rqs_bin<!INV>(xv, K, p);
-            if (!INV) {
-              float yv, l;
-              rqs_forward_eval(xv, bin, yv, l);
-              *xp = yv;
-              ldv = l;
-            } else {
-              *xp = rqs_inverse_eval(xv, bin);
-            }
+        // Run the spline for every pair of transformed dims whose 2*S parameter
+        // rows are complete, except after the last tile: the pairs left then
+        // run below, after the loop, when the hidden activations are dead.
+        if (o + 1 < T_last) {
+          while (next_d < dt) {
+            const int end = (next_d + 2 < dt) ? next_d + 2 : dt;
+            if (end * S > (o + 1) * 32) break;
+            spline_pair<INV>(ring, xs, s, hh, next_d, end, S, K, mask, cth, norm, rnorm, rot, D, ldc);
+            next_d += 2;
           }
-          wave_lds_sync();
-          if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139)
-            const float other = __shfl_xor(ldv, 32);
-            const float first = hh == 0 ? ldv : other;
-            const float second = hh == 0 ? other : ldv;
-            ldc = ldc + first;
-            if (end - next_d == 2) ldc = ldc + second;
-          }
-          next_d += 2;
         }
+      }
+      while (next_d < dt) {
+        const int end = (next_d + 2 < dt) ? next_d + 2 : dt;
+        spline_pair<INV>(ring, xs, s, hh, next_d, end, S, K, mask, cth, norm, rnorm, rot, D, ldc);
+        next_d += 2;
       }
       if (!INV) ld = ld + ldc;  // Chain: log_det += ld (bijectors.py:110)
     }
@@ -685,6 +710,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       }
       d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
       d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
+      d.first_chunk = op.n_hidden > 1 ? d.w[1] : d.w[op.n_hidden];
     } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
       d.sb = take(8 * desc.dim);
     }

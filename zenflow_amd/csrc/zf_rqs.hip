@@ -113,48 +113,6 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
   }
 }
 
-// Bin search + gather over knots held in registers (compile-time K, so every
-// w[j]/h[j] index is static); same count semantics as zf_spline.h::rqs_bin.
-template <bool FWD, int K>
-__device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], const float (&h)[K],
-                                               const float* sl) {
-  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
-  int cnt = 0, sel = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const float kk = FWD ? xk : yk;
-    if (kk <= v) { ++cnt; sel = j; sxk = xk; syk = yk; sw = w[j]; sh = h[j]; }
-    xk = xk + w[j];
-    yk = yk + h[j];
-  }
-  {
-    const float kk = FWD ? xk : yk;
-    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; sw = qnan(); sh = qnan(); }
-  }
-  int idx = cnt - 1;
-  idx = idx < 0 ? 0 : (idx > K ? K : idx);
-  if (idx != sel) {  // non-monotone knots (never from normalize_spline_params)
-    xk = 0.f; yk = 0.f;
-    sw = qnan(); sh = qnan();
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (j == idx) { sw = w[j]; sh = h[j]; }
-      if (j < idx) { xk = xk + w[j]; yk = yk + h[j]; }
-    }
-    sxk = xk; syk = yk; sel = idx;
-  }
-  RqsBin b;
-  b.xk = sxk;
-  b.yk = syk;
-  b.w = sw;
-  b.h = sh;
-  b.dk = (sel == 0 || sel == K) ? 1.0f : sl[sel - 1];
-  b.dkp1 = (sel + 1 < K) ? sl[sel] : (sel + 1 == K ? 1.0f : qnan());
-  b.sk = b.h / b.w;
-  b.oob = (v < 0.f) || (v >= 1.f);
-  return b;
-}
-
 // Direct (no-LDS) path for K % 4 == 0: one thread per (row, dim) item reads
 // its own dx/dy rows as K/4 dwordx4 each (a 64-B row per array at K=16; the
 // thread consumes every byte it fetches), keeps the knots in registers and
@@ -186,7 +144,8 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
     h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
   }
   const float v = xin[item];
-  const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, slope + item * (K - 1));
+  const float* slp = slope + item * (K - 1);
+  const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, [&](int j) { return slp[j]; });
   if (FWD) {
     float y, l;
     rqs_forward_eval(v, bn, y, l);

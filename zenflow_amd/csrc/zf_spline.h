@@ -65,6 +65,49 @@ __device__ __forceinline__ RqsBin rqs_bin(float v, int K, const P& p) {
   return b;
 }
 
+// Same bin search + gather over knots held in registers (compile-time K: every
+// w[j] / h[j] index is static).  `slope(j)` returns the derivative at inner
+// knot j+1; only the two the bin needs are requested.
+template <bool FWD, int K, class SL>
+__device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], const float (&h)[K],
+                                               const SL& slope) {
+  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  int cnt = 0, sel = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = j; sxk = xk; syk = yk; sw = w[j]; sh = h[j]; }
+    xk = xk + w[j];
+    yk = yk + h[j];
+  }
+  {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; sw = qnan(); sh = qnan(); }
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  if (idx != sel) {  // non-monotone knots (never from normalize_spline_params)
+    xk = 0.f; yk = 0.f;
+    sw = qnan(); sh = qnan();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j == idx) { sw = w[j]; sh = h[j]; }
+      if (j < idx) { xk = xk + w[j]; yk = yk + h[j]; }
+    }
+    sxk = xk; syk = yk; sel = idx;
+  }
+  RqsBin b;
+  b.xk = sxk;
+  b.yk = syk;
+  b.w = sw;
+  b.h = sh;
+  b.dk = (sel == 0 || sel == K) ? 1.0f : slope(sel - 1);
+  b.dkp1 = (sel + 1 < K) ? slope(sel) : (sel + 1 == K ? 1.0f : qnan());
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+
 // utils.py:121-139 — forward value and per-dim log|dy/dx|.
 __device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
   const float zr = (x - b.xk) / b.w;               // :122
