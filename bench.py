@@ -7,7 +7,7 @@ config — 4D rolling spline coupling flow, K=16 knots, 4 couplings, hidden
 One process per GPU (torch.distributed.run for N>1; torch is only the control
 plane: barrier, max-over-ranks timing, RCCL unique-id broadcast).  A step is
 one log_prob pass over the resident 2^20-row shard: the fused kernel
-(ShiftBounds -> 4x[MLP on fp32 MFMA + RQ spline] -> Normal latent -> NaN->-inf
+(ShiftBounds -> 4x[MLP on MFMA + RQ spline] -> Normal latent -> NaN->-inf
 -> per-block NLL partials), the fp64 NLL reduce and, for N>1, the RCCL
 all-reduce of the NLL.  Rank 0 prints one JSON line."""
 
@@ -26,6 +26,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (no xf32 on gfx950)
+PEAK_BF16_MFMA_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz
+# fp32-accurate GEMM by the three-term bf16 split: 6 bf16 products per fp32 product
+PEAK_BF16X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
 
 WORKLOADS = {
@@ -268,7 +271,9 @@ def main():
 
     fps = flops_per_sample(name)
     achieved = fps * N / (kavg * 1e-3) / 1e12
-    kernel_name = "flow_kernel"
+    variant = prog.kernel_variant
+    kernel_name = "flow_kernel_x3" if variant == "bf16x3" else "flow_kernel"
+    peak = PEAK_BF16X3_TFLOPS if variant == "bf16x3" else PEAK_FP32_MFMA_TFLOPS
     traffic = load_traffic(kernel_name, 1)
     result = {
         "metric": "log_prob samples/sec (+ NLL match) 4D 16-knot 4-layer flow, batch 2^20"
@@ -292,16 +297,20 @@ def main():
             "rows_per_gpu": N,
             "global_batch": N * world,
             "parallelism": f"dp{world} (batch shards, RCCL all-reduce of the fp64 NLL)",
+            "kernel": variant,
         },
         "roofline": {
             "bound": "mfma",
             "achieved": achieved,
-            "peak": PEAK_FP32_MFMA_TFLOPS,
+            "peak": peak,
             "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+            "frac": achieved / peak,
             "traffic": traffic,
             "kernel": f"{kernel_name} (avg {kavg * 1e3:.1f} us over {args.steps} timed launches, HIP events)",
             "alg_flops_per_sample": fps,
+            "peak_basis": "bf16 dense MFMA peak / 6 (three-term split, fp32-equivalent flops)"
+            if variant == "bf16x3" else "fp32 dense MFMA peak",
+            "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
         },
     }
     if mode == "log_prob":

@@ -158,6 +158,16 @@ int zf_flow_create(const zf_flow_desc* desc, const float* blob_host, int64_t blo
                    zf_flow_t** handle);
 int zf_flow_destroy(zf_flow_t* handle);
 
+/* Which fused kernel the handle runs (no reference counterpart: an
+ * implementation detail made observable for tests and benchmarks):
+ * ZF_KERNEL_FP32 (fp32 MFMA, any supported shape) or ZF_KERNEL_BF16X3
+ * (three-term bf16 split on bf16 MFMA, fp32-equivalent accuracy; hidden
+ * widths <= 128 padded to 128, knots 8 or 16, dim <= 5; disabled by the
+ * environment variable ZF_DISABLE_X3=1 at zf_flow_create time).  -1 if h is NULL. */
+#define ZF_KERNEL_FP32 0
+#define ZF_KERNEL_BF16X3 1
+int zf_flow_kernel_variant(const zf_flow_t* h);
+
 /* Device workspace needed by zf_flow_log_prob for N rows. */
 int64_t zf_flow_workspace_bytes(int64_t N);
 

@@ -176,3 +176,61 @@ def test_edge_inputs():
     assert_allclose(lp[fin], ref[fin], rtol=REL, atol=REL)
     case["x"] = np.zeros((0, 4), F32)
     assert gpu_log_prob(case).shape == (0,)
+
+
+# --- kernel variants -----------------------------------------------------------
+# Shapes the bf16x3 kernel takes (hidden <= 128, knots 8/16, dim <= 5) run on
+# it by default; ZF_DISABLE_X3=1 forces the fp32-MFMA kernel, which must stay
+# parity-green on the same shapes.
+
+X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep"]
+
+
+@pytest.mark.parametrize("name", X3_SHAPES + ["cfg5", "small", "odd", "uniform"])
+def test_kernel_selection(name):
+    case = make_case(name, N=8, seed=30)
+    _, bf = _bound(case)
+    want = "bf16x3" if name in X3_SHAPES else "fp32"
+    assert bf.program.kernel_variant == want
+
+
+@pytest.mark.parametrize("name", X3_SHAPES)
+def test_fp32_kernel_parity_when_x3_disabled(name, monkeypatch):
+    monkeypatch.setenv("ZF_DISABLE_X3", "1")
+    case = make_case(name, N=3000, seed=31)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "fp32"
+    check_lp(gpu_log_prob(case), case, f"fp32/{name}")
+
+
+@pytest.mark.parametrize("N", [255, 256, 257, 129, 100003])
+def test_x3_ragged_batches(N):
+    """Block = 256 samples on the bf16x3 kernel: partial blocks, the NLL
+    workspace layout shared with the 128-row fp32 kernel."""
+    from zenflow_amd._lib import DeviceArray
+
+    case = make_case("cfg2", N=N, seed=32)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "bf16x3"
+    xd = DeviceArray.from_numpy(case["x"])
+    nll = DeviceArray((1,), np.float64)
+    lp = bf.log_prob(xd, nll_sum=nll).numpy()
+    assert abs(nll.numpy()[0] - lp.astype(np.float64).sum()) <= 1e-9 * max(1.0, abs(nll.numpy()[0]))
+    if N <= 4096:
+        check_lp(lp, case, f"x3/N={N}")
+
+
+def test_x3_matches_fp32_kernel(monkeypatch):
+    """Both kernels on the same 2^16 rows: equal to within the fp32 parity bar."""
+    from zenflow_amd._lib import DeviceArray
+
+    case = make_case("cfg2", N=1 << 16, seed=33)
+    _, b3 = _bound(case)
+    monkeypatch.setenv("ZF_DISABLE_X3", "1")
+    _, b32 = _bound(case)
+    xd = DeviceArray.from_numpy(case["x"])
+    l3, l32 = b3.log_prob(xd).numpy(), b32.log_prob(xd).numpy()
+    fin = np.isfinite(l3) & np.isfinite(l32)
+    assert np.mean(np.isfinite(l3) != np.isfinite(l32)) <= 1e-3
+    rel = np.abs(l3[fin] - l32[fin]) / np.maximum(1, np.abs(l32[fin]))
+    assert np.quantile(rel, 0.999) <= REL and rel.mean() <= 1e-6

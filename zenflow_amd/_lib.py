@@ -32,6 +32,8 @@ ZF_SB_NONE = 0
 ZF_SB_BOTH = 1
 ZF_SB_LOWER = 2
 ZF_SB_UPPER = 3
+ZF_KERNEL_FP32 = 0
+ZF_KERNEL_BF16X3 = 1
 
 
 class ZfOpDesc(C.Structure):
@@ -97,6 +99,7 @@ SIGNATURES = {
     "zf_flow_plan": (_int, [C.POINTER(ZfFlowDesc), C.POINTER(_i64)]),
     "zf_flow_create": (_int, [C.POINTER(ZfFlowDesc), _vp, _i64, C.POINTER(_vp)]),
     "zf_flow_destroy": (_int, [_vp]),
+    "zf_flow_kernel_variant": (_int, [_vp]),
     "zf_flow_workspace_bytes": (_i64, [_i64]),
     "zf_flow_log_prob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "zf_flow_log_prob_segment": (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -20,8 +20,7 @@
 //     (lane = sample, conflict-free), where one lane per (sample, dim) runs
 //     normalize_spline_params + bin search + RQ spline + log-det in registers;
 //   * per-sample state (D floats) lives in LDS; Roll is an index rotation.
-#include "zf_internal.h"
-#include "zf_spline.h"
+#include "zf_flow_dev.h"
 
 #include <cmath>
 #include <cstring>
@@ -30,103 +29,8 @@
 namespace zf {
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-constexpr int kWaves = 4;               // waves per block
-constexpr int kTile = 32;               // samples per wave
+constexpr int kWaves = 4;  // waves per block
 constexpr int kBlockRows = kWaves * kTile;
-constexpr int kMaxOps = 64;
-
-struct DevOp {
-  int kind, shift, K, S;
-  int n_hidden, dt, dc, DC;
-  int KS0, T_last, nslot_mask, act;
-  long long w[17];
-  long long b[17];
-  long long bn;
-  long long sb;
-  long long first_chunk;   // blob offset of this NSC's first streamed weight chunk
-};
-
-struct DevFlow {
-  int D, C, latent, n_ops;
-  int HP, nslot, per_wave, pad;
-  float lat_c0, lat_c1, lat_c2, lat_c3;
-  DevOp ops[kMaxOps];
-};
-
-__device__ __forceinline__ void wave_lds_sync() {
-  // LDS ops of one wave execute in order; this only stops the compiler from
-  // moving LDS accesses across the exchange point.
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// flax.linen.swish = x * sigmoid(x) = x / (1 + exp(-x)) (bijectors.py:319).
-// exp(-x) = 2^t * (1 + lo*ln2) with t = -x*log2e rounded and lo its exact
-// residual (fma) plus the log2e tail: ~1 ulp instead of the |x|*6e-8 relative
-// error of a bare v_exp_f32(-x*log2e); the reciprocal gets one Newton step.
-// 0: v * rcp(1 + 2^(-v*log2e))  (6 VALU, ~|v|*6e-8 relative error)
-// 1: compensated exp argument + Newton reciprocal (~1 ulp, 16 VALU)
-// 2: expf + IEEE division (reference form)
-// All three give the same mean log_prob error as the fp32 oracle
-// (scripts/diag_parity.py); 0 is the default.
-#ifndef ZF_SWISH_MODE
-#define ZF_SWISH_MODE 0
-#endif
-__device__ __forceinline__ float swish(float v) {
-#if ZF_SWISH_MODE == 0
-  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.44269504f));
-#elif ZF_SWISH_MODE == 2
-  return v * (1.0f / (1.0f + expf(-v)));
-#endif
-  constexpr float kL2E = 1.44269502162933349609375f;  // fp32(log2 e)
-  constexpr float kL2ELo = 1.925963033500011e-08f;    // log2 e - kL2E
-  constexpr float kLn2 = 0.693147180559945f;
-  const float nv = -v;
-  const float t = nv * kL2E;
-  const float lo = __builtin_fmaf(nv, kL2E, -t) + nv * kL2ELo;
-  const float p = __builtin_amdgcn_exp2f(t);
-  const float e = (p == INFINITY) ? p : __builtin_fmaf(p, lo * kLn2, p);
-  const float d = 1.0f + e;
-  float r = __builtin_amdgcn_rcpf(d);
-  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
-  return v * r;
-}
-
-// 1/x to ~0.5 ulp: hardware reciprocal + one Newton step.
-__device__ __forceinline__ float rcp_refined(float x) {
-  float r = __builtin_amdgcn_rcpf(x);
-  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
-}
-
-// x / d given r = rcp_refined(d): one residual correction of the product
-// makes the quotient correctly rounded for these (normal, non-overflowing)
-// operands — the IEEE division the reference performs, at a third of the cost.
-__device__ __forceinline__ float div_cr(float x, float d, float r) {
-  const float q = x * r;
-  return __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
-}
-
-// squareplus (utils.py:18-20) with a residual-corrected hardware square root
-// (x^2 + 4 >= 4: never denormal); matches the correctly rounded sqrtf.
-__device__ __forceinline__ float squareplus_fast(float x) {
-  const float a = x * x + 4.0f;
-  float sq = __builtin_amdgcn_sqrtf(a);
-  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * __builtin_amdgcn_rcpf(sq), sq);
-  return 0.5f * (x + sq);
-}
-
-// Bias of one 32-row output tile for this lane's 16 accumulator rows (packed
-// [2 lane halves][16]).  Callers issue it BEFORE the tile's weight stream:
-// vmcnt retires in order, so a bias load issued after the prefetch of the
-// next weight chunk would make its consumer drain that prefetch too.
-__device__ __forceinline__ void bias_tile(const float* __restrict__ bt, int hh, floatx4 (&b)[4]) {
-  const floatx4* p = reinterpret_cast<const floatx4*>(bt + hh * 16);
-#pragma unroll
-  for (int r4 = 0; r4 < 4; ++r4) b[r4] = p[r4];
-}
 
 // One 32-row output tile of a Dense layer on MFMA: acc = W^T[tile] . H over
 // the T input tiles (activations hb: unit rows in registers, sample on the
@@ -162,11 +66,6 @@ __device__ __forceinline__ floatx16 mfma_tile(const floatx4* __restrict__ p,
     }
   }
   return acc;
-}
-
-__device__ __forceinline__ int pmod(int a, int m) {
-  int r = a % m;
-  return r < 0 ? r + m : r;
 }
 
 // Raw conditioner outputs of one (sample, transformed dim) in the LDS ring:
@@ -271,7 +170,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
   const long long row = ((long long)blockIdx.x * kWaves + wave) * kTile + s;
   const bool valid = row < N;
 
-  for (int d = hh; d < D; d += 2) xs[d * 32 + s] = valid ? xin[row * D + d] : 0.f;
+  load_state(xs, xin, row, valid, D, s, hh);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;  // logical dim j is stored in column (j + rot) mod D
   wave_lds_sync();
@@ -285,80 +184,16 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
     if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
       rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
-      const float* sb = blob + op.sb;
-      if (!INV) {  // bijectors.py:181-208 (eval branch of :261-273)
-        float ldsb = 0.f;
-        for (int i = 0; i < D; ++i) {
-          const int p = pmod(i + rot, D);
-          const float v = xs[p * 32 + s];
-          const int mode = (int)sb[8 * i];
-          const float a = sb[8 * i + 1], b = sb[8 * i + 2], xmin = sb[8 * i + 3];
-          const float mul = sb[8 * i + 5], logmul = sb[8 * i + 6];
-          float z, l;
-          if (mode == ZF_SB_BOTH) {  // :187-192
-            z = (v - a) * mul;
-            l = logmul;
-          } else {
-            float t = v;
-            if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);  // safe_log :430
-            if (mode == ZF_SB_UPPER) t = logf((b - v) + 1.17549435e-38f);
-            const float zr = (t - xmin) * mul;
-            z = (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);  // :272 clip
-            l = (mode == ZF_SB_NONE) ? logmul : logmul - t;    // :197, :202
-          }
-          ldsb = ldsb + l;
-          if (hh == 0) xs[p * 32 + s] = z;
-        }
-        ld = ld + ldsb;
-      } else {  // bijectors.py:210-240
-        for (int i = 0; i < D; ++i) {
-          const int p = pmod(i + rot, D);
-          const float zv = xs[p * 32 + s];
-          const int mode = (int)sb[8 * i];
-          const float a = sb[8 * i + 1], b = sb[8 * i + 2];
-          const float xmin = sb[8 * i + 3], xmax = sb[8 * i + 4];
-          float xv;
-          if (mode == ZF_SB_BOTH) {
-            xv = zv * b + (1.f - zv) * a;
-          } else {
-            const float t = zv * xmax + (1.f - zv) * xmin;
-            xv = (mode == ZF_SB_LOWER) ? expf(t) + a : (mode == ZF_SB_UPPER ? b - expf(t) : t);
-          }
-          if (hh == 0) xs[p * 32 + s] = xv;
-        }
-      }
-      wave_lds_sync();
+      shift_bounds_op<INV>(blob + op.sb, xs, s, hh, rot, D, ld);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
-      const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
-      const int DCp = 2 * KS0;
-      const float* bn = blob + op.bn;
+      const int dt = op.dt;
       {  // first streamed chunk flies while layer 0 runs
         const floatx4* f = reinterpret_cast<const floatx4*>(blob + op.first_chunk) + lane;
 #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) wc[r4] = f[r4 * 64];
       }
       floatx16 hb[T];
-#pragma unroll
-      for (int o = 0; o < T; ++o) hb[o] = floatx16{0};
-      // Layer 0: u = BatchNorm(hstack(xc, c)) (:341-342), one MFMA k-step per 2 inputs.
-      for (int ks = 0; ks < KS0; ++ks) {
-        const int k = 2 * ks + hh;
-        float v = 0.f;
-        if (k < dc) v = xs[pmod(dt + k + rot, D) * 32 + s];
-        else if (k < DC) v = valid ? cin[row * C + (k - dc)] : 0.f;
-        const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
-        const float* w0 = blob + op.w[0] + ks * 64 + lane;
-#pragma unroll
-        for (int o = 0; o < T; ++o)
-          hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
-      }
-#pragma unroll
-      for (int o = 0; o < T; ++o) {
-        floatx4 bv[4];
-        bias_tile(blob + op.b[0] + o * 32, hh, bv);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + bv[r >> 2][r & 3]);
-      }
+      layer0<T>(op, blob, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
       // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.  The last
       // tile of each layer prefetches the next layer's first chunk.
       for (int l = 1; l < op.n_hidden; ++l) {
@@ -382,11 +217,8 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
       const int K = op.K, S = op.S, mask = op.nslot_mask;
       const floatx4* wl = reinterpret_cast<const floatx4*>(blob + op.w[op.n_hidden]) + lane;
       const float* bl = blob + op.b[op.n_hidden];
-      // utils.py:32-34: c and 1 + c*n are Python floats (fp64), rounded to fp32 on use
-      const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
-      const float cth = (float)c64;
-      const float norm = (float)(1.0 + c64 * (double)K);
-      const float rnorm = rcp_refined(norm);
+      const KnotConsts kc(K);
+      const float cth = kc.c, norm = kc.norm, rnorm = kc.rnorm;
       int next_d = 0;
       float ldc = 0.f;
       const int T_last = op.T_last;
@@ -423,58 +255,8 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
     }
   }
 
-  // ---- epilogue -----------------------------------------------------------
-  if (lp_out != nullptr) {
-    // latent.log_prob(z) (distributions.py:16-33) + log_det (flow.py:46)
-    const int lt = F->latent;
-    const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
-    float lat = 0.f;
-    for (int j = 0; j < D; ++j) {
-      const float v = xs[pmod(j + rot, D) * 32 + s];
-      float t;
-      if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
-        // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
-        const float dv = v - 0.5f;
-        t = (c0 + (dv * dv) / c1) / -2.0f;
-        if (lt == ZF_LATENT_TRUNCNORM) {  // - log mass; -inf outside [-5, 5] sigma
-          t = t - c2;
-          const float xsd = dv / 0.1f;
-          if (xsd < -5.f || xsd > 5.f) t = -INFINITY;
-        }
-      } else if (lt == ZF_LATENT_BETA) {
-        // -betaln(a,a) + xlogy(a-1, x) + xlog1py(a-1, -x); -inf outside [0, 1]
-        const float l1 = (c1 == 0.f) ? 0.f : c1 * logf(v);
-        const float l2 = (c1 == 0.f) ? 0.f : c1 * log1pf(-v);
-        t = c0 + (l1 + l2);
-        if (v > 1.f || v < 0.f) t = -INFINITY;
-      } else {  // uniform
-        t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
-      }
-      lat = lat + t;
-    }
-    float lp = lat + ld;
-    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): +-inf -> +-max finite
-    if (lp != lp) lp = -INFINITY;
-    else if (lp == INFINITY) lp = 3.40282347e38f;
-    else if (lp == -INFINITY) lp = -3.40282347e38f;
-    if (valid && hh == 0) lp_out[row] = lp;
-    if (block_partial != nullptr) {
-      double v = (valid && hh == 0) ? (double)lp : 0.0;
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-      if (lane == 0) s_part[wave] = v;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double acc = 0.0;
-        for (int w = 0; w < kWaves; ++w) acc += s_part[w];
-        block_partial[blockIdx.x] = acc;
-      }
-    }
-  }
-  if (y_out != nullptr && valid) {
-    for (int j = hh; j < D; j += 2) y_out[row * D + j] = xs[pmod(j + rot, D) * 32 + s];
-  }
-  if (ld_out != nullptr && valid && hh == 0) ld_out[row] = ld;
+  flow_epilogue<kWaves>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, 0,
+                        y_out, ld_out, s_part);
 }
 
 // Deterministic fixed-order sum of per-block partials -> out[0].
@@ -572,6 +354,8 @@ struct zf_flow {
   std::vector<float> packed;  // device blob (host copy)
   zf::DevFlow* d_desc = nullptr;
   float* d_blob = nullptr;
+  void* d_x3 = nullptr;       // bf16x3 weight-group stream (x3 kernel), or null
+  int x3_K = 0;
   int device = 0;
 };
 
@@ -691,6 +475,8 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off = zf::round_up64(off + n, 4); return o; };
   int nslot = 1;
+  int x3K = 0;
+  const bool x3 = zf::x3_eligible(desc, HP, &x3K);
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     zf::DevOp& d = F.ops[i];
@@ -711,6 +497,8 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
       d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
       d.first_chunk = op.n_hidden > 1 ? d.w[1] : d.w[op.n_hidden];
+      d.x3 = -1;
+      if (x3) d.x3_blast = take((int64_t)zf::x3_last_tiles(x3K) * 32);
     } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
       d.sb = take(8 * desc.dim);
     }
@@ -774,8 +562,17 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       }
     }
   }
+  std::vector<uint16_t> x3s;
+  if (x3) {
+    zf::x3_pack(desc, nat, F, P, x3s);
+    F.x3_ok = 1;
+    h->x3_K = x3K;
+  }
   int rcd = ZF_OK;
   hipError_t e = hipGetDevice(&h->device);
+  if (e == hipSuccess && x3) e = hipMalloc(&h->d_x3, x3s.size() * sizeof(uint16_t));
+  if (e == hipSuccess && x3)
+    e = hipMemcpy(h->d_x3, x3s.data(), x3s.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&h->d_desc, sizeof(zf::DevFlow));
   if (e == hipSuccess) e = hipMalloc(&h->d_blob, h->packed.size() * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(h->d_desc, &h->host, sizeof(zf::DevFlow), hipMemcpyHostToDevice);
@@ -794,8 +591,14 @@ int zf_flow_destroy(zf_flow_t* h) {
   if (!h) return ZF_OK;
   if (h->d_desc) (void)hipFree(h->d_desc);
   if (h->d_blob) (void)hipFree(h->d_blob);
+  if (h->d_x3) (void)hipFree(h->d_x3);
   delete h;
   return ZF_OK;
+}
+
+int zf_flow_kernel_variant(const zf_flow_t* h) {
+  if (!h) return -1;
+  return h->host.x3_ok ? ZF_KERNEL_BF16X3 : ZF_KERNEL_FP32;
 }
 
 int64_t zf_flow_workspace_bytes(int64_t N) {
@@ -818,6 +621,15 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
   if (N == 0) return ZF_OK;
   if (!x) return einval("x is NULL");
   if (h->host.C > 0 && !c) return einval("flow is conditional (C=%d) but c is NULL", h->host.C);
+  if (h->host.x3_ok) {
+    X3Launch a;
+    a.desc = h->d_desc; a.blob = h->d_blob; a.x3 = h->d_x3;
+    a.x = x; a.c = c; a.y = y; a.ld_in = ld_in; a.ld_out = ld_out; a.lp = lp; a.part = part;
+    a.nparts = (N + kBlockRows - 1) / kBlockRows;
+    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D;
+    a.stream = (hipStream_t)stream;
+    return launch_flow_x3(a, INV);
+  }
   const int64_t grid = (N + kBlockRows - 1) / kBlockRows;
   if (grid > 0x7fffffffLL) return einval("N too large");
   const size_t lds = sizeof(float) * (size_t)kWaves * h->host.per_wave;

@@ -1,0 +1,311 @@
+// Device-side pieces shared by the two fused flow kernels (zf_flow.hip: fp32
+// MFMA, any width; zf_flow_x3.hip: bf16x3 MFMA with LDS-shared weights): the
+// device flow descriptor, the scalar numerics the reference fixes, and the
+// op steps that do not touch the conditioner GEMMs (ShiftBounds, the
+// BatchNorm + first Dense layer, the latent log_prob epilogue).
+#pragma once
+#include "zf_internal.h"
+#include "zf_spline.h"
+
+#include <cstdint>
+#include <vector>
+
+namespace zf {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 32;  // samples per wave (one MFMA column block)
+constexpr int kMaxOps = 64;
+
+struct DevOp {
+  int kind, shift, K, S;
+  int n_hidden, dt, dc, DC;
+  int KS0, T_last, nslot_mask, act;
+  long long w[17];
+  long long b[17];
+  long long bn;
+  long long sb;
+  long long first_chunk;  // blob offset of this NSC's first streamed weight chunk (fp32 kernel)
+  // bf16x3 kernel: byte offset of this NSC's weight-group stream in the x3
+  // blob, its group count, blob offset of the row-permuted last-layer bias,
+  // and the next NSC op index in forward / inverse execution order (or -1).
+  long long x3;
+  long long x3_blast;
+  int x3_groups, x3_tlast;
+  int x3_next[2];
+};
+
+struct DevFlow {
+  int D, C, latent, n_ops;
+  int HP, nslot, per_wave, x3_ok;
+  float lat_c0, lat_c1, lat_c2, lat_c3;
+  DevOp ops[kMaxOps];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS ops of one wave execute in order; this only stops the compiler from
+  // moving LDS accesses across the exchange point.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// flax.linen.swish = x * sigmoid(x) = x / (1 + exp(-x)) (bijectors.py:319).
+// 0: v * rcp(1 + 2^(-v*log2e))  (6 VALU, ~|v|*6e-8 relative error)
+// 1: compensated exp argument (exact residual of t = -x*log2e plus the log2e
+//    tail) + Newton reciprocal (~1 ulp, 16 VALU)
+// 2: expf + IEEE division (reference form)
+// All three give the same mean log_prob error as the fp32 oracle
+// (scripts/diag_parity.py); 0 is the default.
+#ifndef ZF_SWISH_MODE
+#define ZF_SWISH_MODE 0
+#endif
+__device__ __forceinline__ float swish(float v) {
+#if ZF_SWISH_MODE == 0
+  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.44269504f));
+#elif ZF_SWISH_MODE == 2
+  return v * (1.0f / (1.0f + expf(-v)));
+#else
+  constexpr float kL2E = 1.44269502162933349609375f;  // fp32(log2 e)
+  constexpr float kL2ELo = 1.925963033500011e-08f;    // log2 e - kL2E
+  constexpr float kLn2 = 0.693147180559945f;
+  const float nv = -v;
+  const float t = nv * kL2E;
+  const float lo = __builtin_fmaf(nv, kL2E, -t) + nv * kL2ELo;
+  const float p = __builtin_amdgcn_exp2f(t);
+  const float e = (p == INFINITY) ? p : __builtin_fmaf(p, lo * kLn2, p);
+  const float d = 1.0f + e;
+  float r = __builtin_amdgcn_rcpf(d);
+  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+  return v * r;
+#endif
+}
+
+// 1/x to ~0.5 ulp: hardware reciprocal + one Newton step.
+__device__ __forceinline__ float rcp_refined(float x) {
+  float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+}
+
+// x / d given r = rcp_refined(d): one residual correction of the product
+// makes the quotient correctly rounded for these (normal, non-overflowing)
+// operands — the IEEE division the reference performs, at a third of the cost.
+__device__ __forceinline__ float div_cr(float x, float d, float r) {
+  const float q = x * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
+}
+
+// squareplus (utils.py:18-20) with a residual-corrected hardware square root
+// (x^2 + 4 >= 4: never denormal); matches the correctly rounded sqrtf.
+__device__ __forceinline__ float squareplus_fast(float x) {
+  const float a = x * x + 4.0f;
+  float sq = __builtin_amdgcn_sqrtf(a);
+  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * __builtin_amdgcn_rcpf(sq), sq);
+  return 0.5f * (x + sq);
+}
+
+// Bias of one 32-row output tile for this lane's 16 accumulator rows (packed
+// [2 lane halves][16]).  Callers issue it BEFORE a tile's weight stream:
+// vmcnt retires in order, so a bias load issued after the prefetch of the
+// next weight chunk would make its consumer drain that prefetch too.
+__device__ __forceinline__ void bias_tile(const float* __restrict__ bt, int hh, floatx4 (&b)[4]) {
+  const floatx4* p = reinterpret_cast<const floatx4*>(bt + hh * 16);
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) b[r4] = p[r4];
+}
+
+__device__ __forceinline__ int pmod(int a, int m) {
+  int r = a % m;
+  return r < 0 ? r + m : r;
+}
+
+// softmax_with_threshold constants (utils.py:32-34): c and 1 + c*n are Python
+// floats (fp64), rounded to fp32 where they meet fp32 arrays.
+struct KnotConsts {
+  float c, norm, rnorm;
+  __device__ __forceinline__ explicit KnotConsts(int K) {
+    const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
+    c = (float)c64;
+    norm = (float)(1.0 + c64 * (double)K);
+    rnorm = rcp_refined(norm);
+  }
+};
+
+// Per-wave state: xs[D][32] (column p = stored dim, lane = sample).
+__device__ __forceinline__ void load_state(float* xs, const float* __restrict__ xin, long long row,
+                                           bool valid, int D, int s, int hh) {
+  for (int d = hh; d < D; d += 2) xs[d * 32 + s] = valid ? xin[row * D + d] : 0.f;
+}
+
+// ShiftBounds on the state (bijectors.py:181-208 forward, eval branch of
+// :261-273; :210-240 inverse).  `sb` is the packed [D][8] row block.
+template <bool INV>
+__device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, float* xs, int s, int hh,
+                                                int rot, int D, float& ld) {
+  if (!INV) {
+    float ldsb = 0.f;
+    for (int i = 0; i < D; ++i) {
+      const int p = pmod(i + rot, D);
+      const float v = xs[p * 32 + s];
+      const int mode = (int)sb[8 * i];
+      const float a = sb[8 * i + 1], b = sb[8 * i + 2], xmin = sb[8 * i + 3];
+      const float mul = sb[8 * i + 5], logmul = sb[8 * i + 6];
+      float z, l;
+      if (mode == ZF_SB_BOTH) {  // :187-192
+        z = (v - a) * mul;
+        l = logmul;
+      } else {
+        float t = v;
+        if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);  // safe_log :430
+        if (mode == ZF_SB_UPPER) t = logf((b - v) + 1.17549435e-38f);
+        const float zr = (t - xmin) * mul;
+        z = (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);  // :272 clip
+        l = (mode == ZF_SB_NONE) ? logmul : logmul - t;    // :197, :202
+      }
+      ldsb = ldsb + l;
+      if (hh == 0) xs[p * 32 + s] = z;
+    }
+    ld = ld + ldsb;
+  } else {
+    for (int i = 0; i < D; ++i) {
+      const int p = pmod(i + rot, D);
+      const float zv = xs[p * 32 + s];
+      const int mode = (int)sb[8 * i];
+      const float a = sb[8 * i + 1], b = sb[8 * i + 2];
+      const float xmin = sb[8 * i + 3], xmax = sb[8 * i + 4];
+      float xv;
+      if (mode == ZF_SB_BOTH) {
+        xv = zv * b + (1.f - zv) * a;
+      } else {
+        const float t = zv * xmax + (1.f - zv) * xmin;
+        xv = (mode == ZF_SB_LOWER) ? expf(t) + a : (mode == ZF_SB_UPPER ? b - expf(t) : t);
+      }
+      if (hh == 0) xs[p * 32 + s] = xv;
+    }
+  }
+  wave_lds_sync();
+}
+
+// Conditioner input + first Dense (bijectors.py:341-343): u = BatchNorm(
+// hstack(xc, c)), hb = swish(W0^T u + b0) on fp32 MFMA, one k-step per 2
+// inputs.  hb: T accumulator tiles (unit rows in registers, sample on lane).
+template <int T>
+__device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict__ blob, const float* xs,
+                                       const float* __restrict__ cin, long long row, bool valid, int C,
+                                       int rot, int D, int s, int hh, int lane, floatx16 (&hb)[T]) {
+  const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
+  const int DCp = 2 * KS0;
+  const float* bn = blob + op.bn;
+#pragma unroll
+  for (int o = 0; o < T; ++o) hb[o] = floatx16{0};
+  for (int ks = 0; ks < KS0; ++ks) {
+    const int k = 2 * ks + hh;
+    float v = 0.f;
+    if (k < dc) v = xs[pmod(dt + k + rot, D) * 32 + s];
+    else if (k < DC) v = valid ? cin[row * C + (k - dc)] : 0.f;
+    const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
+    const float* w0 = blob + op.w[0] + ks * 64 + lane;
+#pragma unroll
+    for (int o = 0; o < T; ++o)
+      hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
+  }
+#pragma unroll
+  for (int o = 0; o < T; ++o) {
+    floatx4 bv[4];
+    bias_tile(blob + op.b[0] + o * 32, hh, bv);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + bv[r >> 2][r & 3]);
+  }
+}
+
+// latent.log_prob(z) + log_det, nan_to_num (flow.py:41-48;
+// distributions.py:16-33), block partial of sum(log_prob) for the NLL, and
+// the optional y / log_det outputs.  Partials: block b writes part[b*pstride]
+// (and zero into the pstride-1 slots after it that are < nparts), so every
+// kernel shape leaves the same ceil(N/128)-entry workspace for reduce.
+template <int NW>
+__device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, const float* xs, int s,
+                                              int hh, int lane, int wave, int rot, int D, long long row,
+                                              bool valid, float ld, float* __restrict__ lp_out,
+                                              double* __restrict__ block_partial, int pstride,
+                                              long long nparts, float* __restrict__ y_out,
+                                              float* __restrict__ ld_out, double* s_part) {
+  if (lp_out != nullptr) {
+    const int lt = F->latent;
+    const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
+    float lat = 0.f;
+    for (int j = 0; j < D; ++j) {
+      const float v = xs[pmod(j + rot, D) * 32 + s];
+      float t;
+      if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
+        // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
+        const float dv = v - 0.5f;
+        t = (c0 + (dv * dv) / c1) / -2.0f;
+        if (lt == ZF_LATENT_TRUNCNORM) {  // - log mass; -inf outside [-5, 5] sigma
+          t = t - c2;
+          const float xsd = dv / 0.1f;
+          if (xsd < -5.f || xsd > 5.f) t = -INFINITY;
+        }
+      } else if (lt == ZF_LATENT_BETA) {
+        // -betaln(a,a) + xlogy(a-1, x) + xlog1py(a-1, -x); -inf outside [0, 1]
+        const float l1 = (c1 == 0.f) ? 0.f : c1 * logf(v);
+        const float l2 = (c1 == 0.f) ? 0.f : c1 * log1pf(-v);
+        t = c0 + (l1 + l2);
+        if (v > 1.f || v < 0.f) t = -INFINITY;
+      } else {  // uniform
+        t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
+      }
+      lat = lat + t;
+    }
+    float lp = lat + ld;
+    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): +-inf -> +-max finite
+    if (lp != lp) lp = -INFINITY;
+    else if (lp == INFINITY) lp = 3.40282347e38f;
+    else if (lp == -INFINITY) lp = -3.40282347e38f;
+    if (valid && hh == 0) lp_out[row] = lp;
+    if (block_partial != nullptr) {
+      double v = (valid && hh == 0) ? (double)lp : 0.0;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      if (lane == 0) s_part[wave] = v;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double acc = 0.0;
+        for (int w = 0; w < NW; ++w) acc += s_part[w];
+        const long long b0 = (long long)blockIdx.x * pstride;
+        block_partial[b0] = acc;
+        for (int k = 1; k < pstride; ++k)
+          if (b0 + k < nparts) block_partial[b0 + k] = 0.0;
+      }
+    }
+  }
+  if (y_out != nullptr && valid) {
+    for (int j = hh; j < D; j += 2) y_out[row * D + j] = xs[pmod(j + rot, D) * 32 + s];
+  }
+  if (ld_out != nullptr && valid && hh == 0) ld_out[row] = ld;
+}
+
+// Host-side entry of the bf16x3 kernel (zf_flow_x3.hip).
+struct X3Launch {
+  const DevFlow* desc;
+  const float* blob;
+  const void* x3;
+  const float *x, *c;
+  float* y;
+  const float* ld_in;
+  float *ld_out, *lp;
+  double* part;
+  long long nparts;
+  int op_begin, op_end;
+  long long N;
+  int K, D;
+  hipStream_t stream;
+};
+constexpr int kX3Rows = 256;  // samples per bf16x3 block (8 waves x 32)
+int launch_flow_x3(const X3Launch& a, bool inverse);
+bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
+int x3_last_tiles(int K);
+void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* packed,
+             std::vector<uint16_t>& stream);
+
+}  // namespace zf

@@ -1,0 +1,435 @@
+// Fused flow kernel, bf16x3 variant: the same op chain as flow_kernel
+// (zf_flow.hip) with the conditioner's streamed Dense layers (hidden ->
+// hidden and hidden -> spline parameters) on v_mfma_f32_32x32x16_bf16 using
+// the three-term bf16 split of both operands (x = hi + mid + lo, each an RNE
+// bf16 of the remaining residual) and six products per k-step,
+//   mid*mid + hi*lo + lo*hi + hi*mid + mid*hi + hi*hi   (small terms first),
+// which reproduces an fp32 dot product to ~1e-7 relative (verified on the
+// GPU by tests/hip/mfma_bf16x3_layout.hip) at 16/6 = 2.7x the fp32-MFMA rate.
+//
+// Execution model (DESIGN.md §bf16x3 kernel):
+//   * 8 waves x 32 samples = 256 samples per block, one block per CU (2 waves
+//     per SIMD).  The weight fragments (pre-split hi/mid/lo bf16, packed in
+//     exactly the per-lane order the MFMA A operand wants) are shared by the
+//     8 waves through LDS: each Dense layer is a sequence of "groups" (half
+//     of the layer's input rows for all output tiles; 48 KiB for a 128x128
+//     layer) that the block DMAs global->LDS (global_load_lds_dwordx4) one
+//     group ahead into a double buffer, so every weight byte crosses L2->CU
+//     once per 256 samples instead of once per 32;
+//   * the B operand is the previous layer's f32 accumulator tile, split to
+//     bf16x3 in registers (accumulator-as-operand: k-step s of a tile uses
+//     accumulator registers 8s..8s+7; A is packed with the same k order);
+//   * the last layer's rows are permuted so that lane half h of every output
+//     tile holds 16 consecutive spline parameters of transformed dim h: the
+//     whole normalize_spline_params + bin search + RQ spline runs from
+//     registers, no LDS ring;
+//   * layer 0 (BatchNorm'd conditioning inputs, 1-2 k-steps), ShiftBounds,
+//     Roll and the latent epilogue are the fp32 kernel's (zf_flow_dev.h).
+// Eligibility (host, x3_eligible): hidden widths padded to 128, knots 8 or
+// 16, at most 2 transformed dims (dim <= 5).  Everything else, and
+// ZF_DISABLE_X3=1, runs flow_kernel.
+#include "zf_flow_dev.h"
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace zf {
+namespace {
+
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kX3Waves = kX3Rows / kTile;  // 8
+constexpr int kX3T = 4;                     // hidden tiles (hidden padded to 128)
+constexpr int kHidGroup = 2 * 2 * kX3T * 3 * 1024;  // bytes: [tl][s][o][part] x 1 KiB
+constexpr int kLastGroupPerTile = 2 * 2 * 3 * 1024;
+constexpr int kX3Buf = kHidGroup;           // one LDS weight buffer
+
+// Regs 8s..8s+7 of an accumulator tile -> hi / mid / lo bf16x8 (RNE each).
+template <int S>
+__device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm, bf16x8& bl) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx2 x = {v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
+    const bf16x2 h = __builtin_convertvector(x, bf16x2);
+    const floatx2 r = x - __builtin_convertvector(h, floatx2);
+    const bf16x2 m = __builtin_convertvector(r, bf16x2);
+    const floatx2 r2 = r - __builtin_convertvector(m, floatx2);
+    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
+    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
+    bm[2 * i] = m[0]; bm[2 * i + 1] = m[1];
+    bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
+  }
+}
+
+__device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                          const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
+                                          floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// One weight group from LDS: input tiles 2Q, 2Q+1 (4 k-steps of 16) into
+// NOUT output tiles.  Block (tl, s, o, part) is 1 KiB at
+// (((tl*2 + s)*NOUT + o)*3 + part) KiB; lane l's 16 bytes at l*16.
+template <int NOUT, int Q>
+__device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT],
+                                         int lane) {
+  const char* lb = buf + lane * 16;
+#pragma unroll
+  for (int tl = 0; tl < 2; ++tl) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bh, bm, bl;
+      if (s == 0) split8<0>(hb[2 * Q + tl], bh, bm, bl);
+      else split8<1>(hb[2 * Q + tl], bh, bm, bl);
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        const char* a = lb + ((((tl * 2 + s) * NOUT + o) * 3) << 10);
+        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
+        const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
+        acc[o] = mfma3(ah, am, al, bh, bm, bl, acc[o]);
+      }
+    }
+  }
+}
+
+// Group stream cursor: the group most recently issued (op index + group).
+struct X3Cursor {
+  int op, g;
+};
+
+__device__ __forceinline__ void group_span(const DevOp& op, int g, long long& off, int& pieces) {
+  const int nhid = 2 * (op.n_hidden - 1);
+  if (g < nhid) {
+    off = op.x3 + (long long)g * kHidGroup;
+    pieces = kHidGroup >> 10;
+  } else {
+    off = op.x3 + (long long)nhid * kHidGroup + (long long)(g - nhid) * op.x3_tlast * kLastGroupPerTile;
+    pieces = (op.x3_tlast * kLastGroupPerTile) >> 10;
+  }
+}
+
+// Issue the DMA of one group into an LDS buffer: 1 KiB pieces (one
+// global_load_lds_dwordx4 per wave: wave-uniform LDS base, lane*16 implied)
+// spread over the block's waves.
+__device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave,
+                                       int lane) {
+  for (int p = wave; p < pieces; p += kX3Waves)
+    __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
+}
+
+// Advance the cursor to the next group in execution order within
+// [op_begin, op_end) and DMA it into `dst`; no-op at the end of the stream.
+template <bool INV>
+__device__ __forceinline__ void x3_issue_next(const DevFlow* __restrict__ F, const char* __restrict__ x3,
+                                              X3Cursor& cur, int op_begin, int op_end, char* dst, int wave,
+                                              int lane) {
+  if (cur.op < 0) return;
+  int op = cur.op, g = cur.g + 1;
+  if (g >= F->ops[op].x3_groups) {
+    op = F->ops[op].x3_next[INV ? 1 : 0];
+    g = 0;
+    if (op < op_begin || op >= op_end) op = -1;
+  }
+  cur.op = op;
+  cur.g = g;
+  if (op < 0) return;
+  long long off;
+  int pieces;
+  group_span(F->ops[op], g, off, pieces);
+  x3_dma(x3 + off, dst, pieces, wave, lane);
+}
+
+// Wait for the group in buffer `buf` (issued one step earlier by every wave),
+// release the other buffer, prefetch the next group into it, then run the
+// MFMAs of this group.
+template <int NOUT, int Q, bool INV>
+__device__ __forceinline__ void x3_step(const DevFlow* __restrict__ F, const char* __restrict__ x3,
+                                        X3Cursor& cur, int op_begin, int op_end, char* wbuf, int& buf,
+                                        const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int wave,
+                                        int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<INV>(F, x3, cur, op_begin, op_end, wbuf + (buf ^ 1) * kX3Buf, wave, lane);
+  x3_group<NOUT, Q>(wbuf + buf * kX3Buf, hb, acc, lane);
+  buf ^= 1;
+}
+
+template <int K, bool INV>
+__global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
+    const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
+    const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
+    const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
+    double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N) {
+  constexpr int TL = (3 * K - 1 + 15) / 16;  // last-layer tiles: 16 parameters per lane half
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int D = F->D;
+  const int C = F->C;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int s = lane & 31;
+  const int hh = lane >> 5;
+  char* wbuf = lds;  // [2][kX3Buf] weight groups
+  float* xs = reinterpret_cast<float*>(lds + 2 * kX3Buf) + wave * (32 * D);
+  double* s_part = reinterpret_cast<double*>(lds + 2 * kX3Buf + kX3Waves * 32 * D * 4);
+  const long long row = ((long long)blockIdx.x * kX3Waves + wave) * kTile + s;
+  const bool valid = row < N;
+
+  load_state(xs, xin, row, valid, D, s, hh);
+  float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
+  int rot = 0;
+  wave_lds_sync();
+
+  // First group of the first NSC in execution order goes out now.
+  X3Cursor cur{-1, 0};
+  int buf = 0;
+  {
+    const int nq = op_end - op_begin;
+    for (int q = 0; q < nq; ++q) {
+      const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+      if (F->ops[oi].kind == ZF_OP_NSC) { cur.op = oi; break; }
+    }
+    if (cur.op >= 0) {
+      long long off;
+      int pieces;
+      group_span(F->ops[cur.op], 0, off, pieces);
+      x3_dma(x3 + off, wbuf, pieces, wave, lane);
+    }
+  }
+
+  const KnotConsts kc(K);
+  const int nq = op_end - op_begin;
+  for (int q = 0; q < nq; ++q) {
+    const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+    const DevOp& op = F->ops[oi];
+    const int kind = op.kind;
+    if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
+      rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
+    } else if (kind == ZF_OP_SHIFT_BOUNDS) {
+      shift_bounds_op<INV>(blob + op.sb, xs, s, hh, rot, D, ld);
+    } else {  // ZF_OP_NSC, bijectors.py:329-371
+      floatx16 hb[kX3T];
+      layer0<kX3T>(op, blob, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
+      // Hidden layers 1..n_hidden-1 (:343-345), two groups each.
+      for (int l = 1; l < op.n_hidden; ++l) {
+        floatx16 acc[kX3T];
+#pragma unroll
+        for (int o = 0; o < kX3T; ++o) acc[o] = floatx16{0};
+        x3_step<kX3T, 0, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, acc, wave, lane);
+        x3_step<kX3T, 1, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, acc, wave, lane);
+#pragma unroll
+        for (int o = 0; o < kX3T; ++o) {
+          floatx4 bv[4];
+          bias_tile(blob + op.b[l] + o * 32, hh, bv);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r] + bv[r >> 2][r & 3]);
+        }
+      }
+      // Last Dense (:346-347): lane half h, tile o, register r = parameter
+      // 16*o + r of transformed dim h.
+      floatx16 pa[TL];
+#pragma unroll
+      for (int o = 0; o < TL; ++o) pa[o] = floatx16{0};
+      x3_step<TL, 0, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, pa, wave, lane);
+      x3_step<TL, 1, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, pa, wave, lane);
+      float P[TL * 16];
+#pragma unroll
+      for (int o = 0; o < TL; ++o) {
+        floatx4 bv[4];
+        bias_tile(blob + op.x3_blast + o * 32, hh, bv);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r] + bv[r >> 2][r & 3];
+      }
+      // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
+      const int dt = op.dt;
+      float ldv = 0.f;
+      if (hh < dt) {
+        float w[K], hg[K];
+        float sx = 0.f, sy = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
+          w[j] = squareplus_fast(P[j]);
+          hg[j] = squareplus_fast(P[K + j]);
+          sx = sx + w[j];
+          sy = sy + hg[j];
+        }
+        const float rsx = rcp_refined(sx), rsy = rcp_refined(sy);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          w[j] = div_cr(div_cr(w[j], sx, rsx) + kc.c, kc.norm, kc.rnorm);
+          hg[j] = div_cr(div_cr(hg[j], sy, rsy) + kc.c, kc.norm, kc.rnorm);
+        }
+        auto slope = [&](int j) {  // derivative at inner knot j+1 (j in [0, K-2])
+          float v = P[2 * K];
+#pragma unroll
+          for (int jj = 1; jj < K - 1; ++jj) v = (j == jj) ? P[2 * K + jj] : v;
+          return squareplus_fast(v);
+        };
+        float* xp = xs + pmod(hh + rot, D) * 32 + s;
+        const float xv = *xp;
+        const RqsBin bin = rqs_bin_regs<!INV, K>(xv, w, hg, slope);
+        if (!INV) {
+          float yv;
+          rqs_forward_eval(xv, bin, yv, ldv);
+          *xp = yv;
+        } else {
+          *xp = rqs_inverse_eval(xv, bin);
+        }
+      }
+      wave_lds_sync();
+      if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139), Chain += (bijectors.py:110)
+        const float other = __shfl_xor(ldv, 32);
+        float ldc = hh == 0 ? ldv : other;
+        if (dt == 2) ldc = ldc + (hh == 0 ? other : ldv);
+        ld = ld + ldc;
+      }
+    }
+  }
+
+  flow_epilogue<kX3Waves>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial,
+                          kX3Rows / 128, nparts, y_out, ld_out, s_part);
+}
+
+uint16_t bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+float bf16_f(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+}  // namespace
+
+// hidden widths padded to 128, one knot count in {8, 16}, <= 2 transformed dims.
+bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
+  const char* env = std::getenv("ZF_DISABLE_X3");
+  if (env && env[0] == '1') return false;
+  if (HP != 128) return false;
+  int K = 0;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    if (K == 0) K = op.knots;
+    if (op.knots != K) return false;
+  }
+  if (K != 8 && K != 16) return false;
+  if (desc.dim / 2 > 2) return false;
+  *K_out = K;
+  return true;
+}
+
+int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
+
+// Pack the group streams (bf16 hi/mid/lo A fragments) of every NSC and the
+// row-permuted last-layer biases (into `packed` at F.ops[i].x3_blast, which
+// the caller allocated with x3_last_tiles(K)*32 floats).
+void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* packed,
+             std::vector<uint16_t>& stream) {
+  stream.clear();
+  int prev = -1;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    F.ops[i].x3_next[0] = F.ops[i].x3_next[1] = -1;
+    if (desc.ops[i].kind != ZF_OP_NSC) continue;
+    if (prev >= 0) { F.ops[prev].x3_next[0] = i; F.ops[i].x3_next[1] = prev; }
+    prev = i;
+  }
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    DevOp& d = F.ops[i];
+    const int dt = desc.dim / 2, K = op.knots, S = 3 * K - 1;
+    const int TL = x3_last_tiles(K);
+    d.x3 = (long long)stream.size() * 2;
+    d.x3_tlast = TL;
+    d.x3_groups = 2 * op.n_hidden;
+    for (int l = 1; l <= op.n_hidden; ++l) {
+      const bool last = (l == op.n_hidden);
+      const int in = op.hidden[l - 1];
+      const int out = last ? dt * S : op.hidden[l];
+      const int NOUT = last ? TL : kX3T;
+      const float* W = nat + op.off_w[l];
+      for (int q = 0; q < 2; ++q)
+        for (int tl = 0; tl < 2; ++tl)
+          for (int s = 0; s < 2; ++s)
+            for (int o = 0; o < NOUT; ++o) {
+              uint16_t part[3][64][8];
+              for (int ln = 0; ln < 64; ++ln)
+                for (int j = 0; j < 8; ++j) {
+                  const int kstep = 2 * (2 * q + tl) + s;
+                  const int k = 16 * kstep + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3);
+                  const int rho = ln & 31;
+                  int col;
+                  if (!last) {
+                    col = 32 * o + rho;
+                    if (col >= out) col = -1;
+                  } else {
+                    const int h = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3), jp = 16 * o + r;
+                    col = (h < dt && jp < S) ? h * S + jp : -1;
+                  }
+                  const float x = (k < in && col >= 0) ? W[(int64_t)k * out + col] : 0.f;
+                  const uint16_t bh = bf16_rne(x);
+                  const float r1 = x - bf16_f(bh);
+                  const uint16_t bm = bf16_rne(r1);
+                  const uint16_t bl = bf16_rne(r1 - bf16_f(bm));
+                  part[0][ln][j] = bh;
+                  part[1][ln][j] = bm;
+                  part[2][ln][j] = bl;
+                }
+              const uint16_t* pp = &part[0][0][0];
+              stream.insert(stream.end(), pp, pp + 3 * 64 * 8);
+            }
+    }
+    // permuted last bias: [o][lane half h][r] = bias[h*S + 16o + r]
+    const float* B = nat + op.off_b[op.n_hidden];
+    for (int o = 0; o < TL; ++o)
+      for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) {
+          const int jp = 16 * o + r;
+          packed[d.x3_blast + (o * 2 + h) * 16 + r] = (h < dt && jp < S) ? B[h * S + jp] : 0.f;
+        }
+  }
+}
+
+size_t x3_lds_bytes(int D) {
+  return (size_t)2 * kX3Buf + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
+}
+
+int launch_flow_x3(const X3Launch& a, bool inverse) {
+  const long long grid = (a.N + kX3Rows - 1) / kX3Rows;
+  if (grid > 0x7fffffffLL) return einval("N too large");
+  const size_t lds = x3_lds_bytes(a.D);
+  if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
+#define ZF_X3(KV, IV)                                                                                 \
+  hipLaunchKernelGGL((flow_kernel_x3<KV, IV>), dim3((unsigned)grid), dim3(kX3Rows * 2), lds, a.stream, \
+                     a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,    \
+                     a.nparts, a.op_begin, a.op_end, a.N)
+  if (a.K == 16) {
+    if (inverse) ZF_X3(16, true); else ZF_X3(16, false);
+  } else if (a.K == 8) {
+    if (inverse) ZF_X3(8, true); else ZF_X3(8, false);
+  } else {
+    return enotsup("bf16x3 kernel: knots must be 8 or 16");
+  }
+#undef ZF_X3
+  ZF_CHECK_LAUNCH("flow_kernel_x3");
+  return ZF_OK;
+}
+
+}  // namespace zf

@@ -131,6 +131,12 @@ class Program:
         self.handle = h.value
         self._ws: Optional[DeviceArray] = None
 
+    @property
+    def kernel_variant(self) -> str:
+        """'bf16x3' or 'fp32': the fused kernel this chain runs (zf_flow_kernel_variant)."""
+        v = L.load_library().zf_flow_kernel_variant(ct.c_void_p(self.handle))
+        return "bf16x3" if v == L.ZF_KERNEL_BF16X3 else "fp32"
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h and L._lib is not None:
