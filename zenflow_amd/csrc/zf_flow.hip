@@ -23,6 +23,7 @@
 #include "zf_flow_dev.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -356,6 +357,7 @@ struct zf_flow {
   float* d_blob = nullptr;
   void* d_x3 = nullptr;       // bf16x3 weight-group stream (x3 kernel), or null
   int x3_K = 0;
+  int x3_variant = 0;         // launch shape of the x3 kernel (zf_flow_x3.hip)
   int device = 0;
 };
 
@@ -477,6 +479,9 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   int nslot = 1;
   int x3K = 0;
   const bool x3 = zf::x3_eligible(desc, HP, &x3K);
+  // Small per-op parameters (ShiftBounds rows, BatchNorm, first Dense,
+  // biases) first, for all ops: the bf16x3 kernel stages [0, small_floats)
+  // in LDS once per block.  The streamed fp32 weight fragments follow.
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     zf::DevOp& d = F.ops[i];
@@ -489,19 +494,23 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       nslot = g.nslot > nslot ? g.nslot : nslot;
       d.bn = take(3 * 2 * g.KS0);
       d.w[0] = take((int64_t)T * g.KS0 * 64);
-      d.b[0] = take((int64_t)T * 32);
-      for (int l = 1; l < op.n_hidden; ++l) {
-        d.w[l] = take((int64_t)T * T * 1024);
-        d.b[l] = take((int64_t)T * 32);
-      }
-      d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
+      for (int l = 0; l < op.n_hidden; ++l) d.b[l] = take((int64_t)T * 32);
       d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
-      d.first_chunk = op.n_hidden > 1 ? d.w[1] : d.w[op.n_hidden];
       d.x3 = -1;
       if (x3) d.x3_blast = take((int64_t)zf::x3_last_tiles(x3K) * 32);
     } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
       d.sb = take(8 * desc.dim);
     }
+  }
+  F.small_floats = (int)off;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    zf::DevOp& d = F.ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    const zf::OpGeom g = zf::nsc_geom(&desc, op);
+    for (int l = 1; l < op.n_hidden; ++l) d.w[l] = take((int64_t)T * T * 1024);
+    d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
+    d.first_chunk = op.n_hidden > 1 ? d.w[1] : d.w[op.n_hidden];
   }
   F.nslot = nslot;
   F.per_wave = zf::round_up(32 * desc.dim, 4) + nslot * 1024;
@@ -564,14 +573,20 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   }
   std::vector<uint16_t> x3s;
   if (x3) {
-    zf::x3_pack(desc, nat, F, P, x3s);
-    F.x3_ok = 1;
-    h->x3_K = x3K;
+    const char* v = std::getenv("ZF_X3_VARIANT");
+    h->x3_variant = (v && v[0] >= '0' && v[0] <= '3') ? v[0] - '0' : 0;
+    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) > 160 * 1024) h->x3_variant = 0;
+    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) <= 160 * 1024) {
+      zf::x3_pack(desc, nat, zf::x3_group_tiles(h->x3_variant), F, P, x3s);
+      F.x3_ok = 1;
+      h->x3_K = x3K;
+    }
   }
+  const bool use_x3 = F.x3_ok != 0;
   int rcd = ZF_OK;
   hipError_t e = hipGetDevice(&h->device);
-  if (e == hipSuccess && x3) e = hipMalloc(&h->d_x3, x3s.size() * sizeof(uint16_t));
-  if (e == hipSuccess && x3)
+  if (e == hipSuccess && use_x3) e = hipMalloc(&h->d_x3, x3s.size() * sizeof(uint16_t));
+  if (e == hipSuccess && use_x3)
     e = hipMemcpy(h->d_x3, x3s.data(), x3s.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&h->d_desc, sizeof(zf::DevFlow));
   if (e == hipSuccess) e = hipMalloc(&h->d_blob, h->packed.size() * sizeof(float));
@@ -626,7 +641,8 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.desc = h->d_desc; a.blob = h->d_blob; a.x3 = h->d_x3;
     a.x = x; a.c = c; a.y = y; a.ld_in = ld_in; a.ld_out = ld_out; a.lp = lp; a.part = part;
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
-    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D;
+    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.variant = h->x3_variant;
+    a.small_floats = h->host.small_floats;
     a.stream = (hipStream_t)stream;
     return launch_flow_x3(a, INV);
   }

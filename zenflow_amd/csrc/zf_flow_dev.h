@@ -39,6 +39,7 @@ struct DevOp {
 struct DevFlow {
   int D, C, latent, n_ops;
   int HP, nslot, per_wave, x3_ok;
+  int small_floats, _pad[3];  // packed blob [0, small_floats): per-op small parameters
   float lat_c0, lat_c1, lat_c2, lat_c3;
   DevOp ops[kMaxOps];
 };
@@ -298,14 +299,15 @@ struct X3Launch {
   long long nparts;
   int op_begin, op_end;
   long long N;
-  int K, D;
+  int K, D, variant, small_floats;
   hipStream_t stream;
 };
-constexpr int kX3Rows = 256;  // samples per bf16x3 block (8 waves x 32)
 int launch_flow_x3(const X3Launch& a, bool inverse);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
-void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* packed,
+int x3_group_tiles(int variant);
+size_t x3_lds_bytes(int variant, int small_floats, int D);
+void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);
 
 }  // namespace zf

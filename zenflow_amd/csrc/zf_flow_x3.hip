@@ -42,11 +42,37 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kX3Waves = kX3Rows / kTile;  // 8
-constexpr int kX3T = 4;                     // hidden tiles (hidden padded to 128)
-constexpr int kHidGroup = 2 * 2 * kX3T * 3 * 1024;  // bytes: [tl][s][o][part] x 1 KiB
-constexpr int kLastGroupPerTile = 2 * 2 * 3 * 1024;
-constexpr int kX3Buf = kHidGroup;           // one LDS weight buffer
+constexpr int kX3T = 4;  // hidden tiles (hidden padded to 128)
+// Bytes of one weight group covering GT input tiles: [tl][s][o][part] x 1 KiB.
+constexpr int group_bytes(int GT, int NOUT) { return GT * 2 * NOUT * 3 * 1024; }
+
+#ifndef ZF_X3_ABLATE
+#define ZF_X3_ABLATE 0
+#endif
+#ifndef ZF_X3_TRACE
+#define ZF_X3_TRACE 0
+#endif
+#if ZF_X3_TRACE
+// Timing probe (tuning builds only): s_memtime stamps of every wave of 4
+// blocks, [block][wave][256] (event id << 48 | time).
+__device__ unsigned long long g_x3_trace[4][8][256];
+__device__ int g_x3_trace_n[4][8];
+__device__ __forceinline__ void x3_mark(int ev) {
+  const int b = blockIdx.x;
+  const int tb = b == 5 ? 0 : b == 1029 ? 1 : b == 2053 ? 2 : b == 3077 ? 3 : -1;
+  if (tb < 0) return;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) {
+    const int n = g_x3_trace_n[tb][w];
+    if (n < 256) g_x3_trace[tb][w][n] = ((unsigned long long)ev << 48) | (t & 0xffffffffffffull);
+    g_x3_trace_n[tb][w] = n + 1;
+  }
+}
+#define X3_MARK(ev) x3_mark(ev)
+#else
+#define X3_MARK(ev) ((void)0)
+#endif
 
 // Regs 8s..8s+7 of an accumulator tile -> hi / mid / lo bf16x8 (RNE each).
 template <int S>
@@ -55,6 +81,12 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
   for (int i = 0; i < 4; ++i) {
     const floatx2 x = {v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
     const bf16x2 h = __builtin_convertvector(x, bf16x2);
+#if ZF_X3_ABLATE & 4
+    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
+    bm[2 * i] = h[0]; bm[2 * i + 1] = h[1];
+    bl[2 * i] = h[0]; bl[2 * i + 1] = h[1];
+    continue;
+#endif
     const floatx2 r = x - __builtin_convertvector(h, floatx2);
     const bf16x2 m = __builtin_convertvector(r, bf16x2);
     const floatx2 r2 = r - __builtin_convertvector(m, floatx2);
@@ -68,6 +100,11 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
                                           floatx16 acc) {
+#if ZF_X3_ABLATE & 8
+  asm volatile("" ::"v"(ah), "v"(am), "v"(al), "v"(bh), "v"(bm), "v"(bl));
+  acc[0] += 1.0f;
+  return acc;
+#endif
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
@@ -76,20 +113,20 @@ __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, co
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
-// One weight group from LDS: input tiles 2Q, 2Q+1 (4 k-steps of 16) into
-// NOUT output tiles.  Block (tl, s, o, part) is 1 KiB at
+// One weight group from LDS: input tiles GT*Q .. GT*Q+GT-1 (2 k-steps of 16
+// each) into NOUT output tiles.  Block (tl, s, o, part) is 1 KiB at
 // (((tl*2 + s)*NOUT + o)*3 + part) KiB; lane l's 16 bytes at l*16.
-template <int NOUT, int Q>
+template <int NOUT, int GT, int Q>
 __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT],
                                          int lane) {
   const char* lb = buf + lane * 16;
 #pragma unroll
-  for (int tl = 0; tl < 2; ++tl) {
+  for (int tl = 0; tl < GT; ++tl) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 bh, bm, bl;
-      if (s == 0) split8<0>(hb[2 * Q + tl], bh, bm, bl);
-      else split8<1>(hb[2 * Q + tl], bh, bm, bl);
+      if (s == 0) split8<0>(hb[GT * Q + tl], bh, bm, bl);
+      else split8<1>(hb[GT * Q + tl], bh, bm, bl);
 #pragma unroll
       for (int o = 0; o < NOUT; ++o) {
         const char* a = lb + ((((tl * 2 + s) * NOUT + o) * 3) << 10);
@@ -107,66 +144,112 @@ struct X3Cursor {
   int op, g;
 };
 
+template <int GT>
 __device__ __forceinline__ void group_span(const DevOp& op, int g, long long& off, int& pieces) {
-  const int nhid = 2 * (op.n_hidden - 1);
+  constexpr int per_layer = kX3T / GT;
+  const int nhid = per_layer * (op.n_hidden - 1);
   if (g < nhid) {
-    off = op.x3 + (long long)g * kHidGroup;
-    pieces = kHidGroup >> 10;
+    off = op.x3 + (long long)g * group_bytes(GT, kX3T);
+    pieces = group_bytes(GT, kX3T) >> 10;
   } else {
-    off = op.x3 + (long long)nhid * kHidGroup + (long long)(g - nhid) * op.x3_tlast * kLastGroupPerTile;
-    pieces = (op.x3_tlast * kLastGroupPerTile) >> 10;
+    const int lb = group_bytes(GT, op.x3_tlast);
+    off = op.x3 + (long long)nhid * group_bytes(GT, kX3T) + (long long)(g - nhid) * lb;
+    pieces = lb >> 10;
   }
 }
 
 // Issue the DMA of one group into an LDS buffer: 1 KiB pieces (one
 // global_load_lds_dwordx4 per wave: wave-uniform LDS base, lane*16 implied)
 // spread over the block's waves.
+template <int NW>
 __device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave,
                                        int lane) {
-  for (int p = wave; p < pieces; p += kX3Waves)
+  if (ZF_X3_ABLATE & 16) return;
+  for (int p = wave; p < pieces; p += NW)
     __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
                                      (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
 }
 
+// Block-wide weight-group pipeline state (every field wave-uniform).
+struct X3Pipe {
+  char* wbuf;      // [NBUF][group bytes] LDS ring
+  int buf;         // ring slot holding the group this wave computes next
+  X3Cursor cur;    // group most recently issued (DMA-issuing waves only)
+  int op_begin, op_end;
+  int lead;        // index of this wave among the NL DMA-issuing waves, or -1
+};
+
 // Advance the cursor to the next group in execution order within
 // [op_begin, op_end) and DMA it into `dst`; no-op at the end of the stream.
-template <bool INV>
+template <int NL, int GT, bool INV>
 __device__ __forceinline__ void x3_issue_next(const DevFlow* __restrict__ F, const char* __restrict__ x3,
-                                              X3Cursor& cur, int op_begin, int op_end, char* dst, int wave,
-                                              int lane) {
-  if (cur.op < 0) return;
-  int op = cur.op, g = cur.g + 1;
+                                              X3Pipe& p, char* dst, int lane) {
+  if (p.cur.op < 0) return;
+  int op = p.cur.op, g = p.cur.g + 1;
   if (g >= F->ops[op].x3_groups) {
     op = F->ops[op].x3_next[INV ? 1 : 0];
     g = 0;
-    if (op < op_begin || op >= op_end) op = -1;
+    if (op < p.op_begin || op >= p.op_end) op = -1;
   }
-  cur.op = op;
-  cur.g = g;
+  p.cur.op = op;
+  p.cur.g = g;
   if (op < 0) return;
   long long off;
   int pieces;
-  group_span(F->ops[op], g, off, pieces);
-  x3_dma(x3 + off, dst, pieces, wave, lane);
+  group_span<GT>(F->ops[op], g, off, pieces);
+  x3_dma<NL>(x3 + off, dst, pieces, p.lead, lane);
 }
 
-// Wait for the group in buffer `buf` (issued one step earlier by every wave),
-// release the other buffer, prefetch the next group into it, then run the
-// MFMAs of this group.
-template <int NOUT, int Q, bool INV>
-__device__ __forceinline__ void x3_step(const DevFlow* __restrict__ F, const char* __restrict__ x3,
-                                        X3Cursor& cur, int op_begin, int op_end, char* wbuf, int& buf,
-                                        const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int wave,
-                                        int lane) {
+// One pipeline step: wait for this wave's DMAs, block barrier (the group in
+// slot `buf` is complete and the slot after it is free), the issuing waves
+// prefetch the next group into the next slot, then this group's MFMAs.
+template <int NL, int GT, int NBUF, int NOUT, int Q, bool INV>
+__device__ __forceinline__ void x3_step(const DevFlow* __restrict__ F, const char* __restrict__ x3, X3Pipe& p,
+                                        const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int lane) {
+  constexpr int kBuf = group_bytes(GT, kX3T);
+  X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  x3_issue_next<INV>(F, x3, cur, op_begin, op_end, wbuf + (buf ^ 1) * kX3Buf, wave, lane);
-  x3_group<NOUT, Q>(wbuf + buf * kX3Buf, hb, acc, lane);
-  buf ^= 1;
+  X3_MARK(2);
+  if constexpr (NBUF == 3) {
+    // Offset half-blocks: the wave whose step ends in a VALU tail (the
+    // layer's last group -> epilogue / spline) issues its MFMAs first, so
+    // that tail overlaps the partner wave's MFMAs on the same SIMD.
+    if constexpr (Q + 1 == kX3T / GT) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+  const int nb = (p.buf + 1 == NBUF) ? 0 : p.buf + 1;
+  if (p.lead >= 0) x3_issue_next<NL, GT, INV>(F, x3, p, p.wbuf + nb * kBuf, lane);
+  x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+  p.buf = nb;
 }
 
-template <int K, bool INV>
-__global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
+// A whole streamed Dense layer: kX3T / GT groups.
+template <int NL, int GT, int NBUF, int NOUT, bool INV, int Q = 0>
+__device__ __forceinline__ void x3_layer(const DevFlow* __restrict__ F, const char* __restrict__ x3, X3Pipe& p,
+                                         const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int lane) {
+  x3_step<NL, GT, NBUF, NOUT, Q, INV>(F, x3, p, hb, acc, lane);
+  if constexpr (Q + 1 < kX3T / GT) x3_layer<NL, GT, NBUF, NOUT, INV, Q + 1>(F, x3, p, hb, acc, lane);
+}
+
+// squareplus with a Newton-corrected reciprocal square root (one
+// transcendental instead of sqrt + rcp): ~0.5 ulp, like sqrtf.
+__device__ __forceinline__ float squareplus_rsq(float x) {
+  const float a = x * x + 4.0f;
+  const float r = __builtin_amdgcn_rsqf(a);
+  float sq = a * r;
+  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * r, sq);
+  return 0.5f * (x + sq);
+}
+
+// PIPE 0: every wave issues DMA pieces and all waves step in lockstep
+// (NBUF = 2).  PIPE 1: the block runs as two half-blocks offset by one
+// group — waves [0, NW/2) issue every DMA and compute group t while waves
+// [NW/2, NW) compute group t-1 (NBUF = 3) — so one half's VALU phases
+// (spline, swish epilogues, layer 0) overlap the other half's MFMAs on the
+// same SIMD.
+template <int K, int NW, int GT, int PIPE, bool INV>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
@@ -175,37 +258,53 @@ __global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int D = F->D;
   const int C = F->C;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar cursor math
   const int lane = threadIdx.x & 63;
   const int s = lane & 31;
   const int hh = lane >> 5;
-  char* wbuf = lds;  // [2][kX3Buf] weight groups
-  float* xs = reinterpret_cast<float*>(lds + 2 * kX3Buf) + wave * (32 * D);
-  double* s_part = reinterpret_cast<double*>(lds + 2 * kX3Buf + kX3Waves * 32 * D * 4);
-  const long long row = ((long long)blockIdx.x * kX3Waves + wave) * kTile + s;
+  constexpr int kBuf = group_bytes(GT, kX3T);
+  constexpr int NBUF = PIPE ? 3 : 2;
+  constexpr int NL = PIPE ? NW / 2 : NW;  // DMA-issuing waves
+  // LDS: [NBUF][kBuf] weight ring | small parameters | [NW][D][32] state | [NW] partials
+  const int small4 = (F->small_floats + 3) & ~3;
+  float* sp = reinterpret_cast<float*>(lds + NBUF * kBuf);
+  float* xs = sp + small4 + wave * (32 * D);
+  double* s_part = reinterpret_cast<double*>(sp + small4 + NW * 32 * D);
+  const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
   const bool valid = row < N;
 
+  X3_MARK(0);
+  {  // small parameters -> LDS (before any DMA is in flight)
+    const floatx4* src = reinterpret_cast<const floatx4*>(blob);
+    floatx4* dst = reinterpret_cast<floatx4*>(sp);
+    for (int i = threadIdx.x; i < small4 / 4; i += NW * 64) dst[i] = src[i];
+  }
   load_state(xs, xin, row, valid, D, s, hh);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;
-  wave_lds_sync();
+  __syncthreads();
 
-  // First group of the first NSC in execution order goes out now.
-  X3Cursor cur{-1, 0};
-  int buf = 0;
-  {
+  X3Pipe pipe;
+  pipe.wbuf = lds;
+  pipe.buf = 0;
+  pipe.cur = X3Cursor{-1, 0};
+  pipe.op_begin = op_begin;
+  pipe.op_end = op_end;
+  pipe.lead = wave < NL ? wave : -1;
+  {  // first group of the first NSC in execution order goes out now
     const int nq = op_end - op_begin;
     for (int q = 0; q < nq; ++q) {
       const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
-      if (F->ops[oi].kind == ZF_OP_NSC) { cur.op = oi; break; }
+      if (F->ops[oi].kind == ZF_OP_NSC) { pipe.cur.op = oi; break; }
     }
-    if (cur.op >= 0) {
+    if (pipe.cur.op >= 0 && pipe.lead >= 0) {
       long long off;
       int pieces;
-      group_span(F->ops[cur.op], 0, off, pieces);
-      x3_dma(x3 + off, wbuf, pieces, wave, lane);
+      group_span<GT>(F->ops[pipe.cur.op], 0, off, pieces);
+      x3_dma<NL>(x3 + off, pipe.wbuf, pieces, pipe.lead, lane);
     }
   }
+  if (PIPE && pipe.lead < 0) __syncthreads();  // trailing half starts one step late
 
   const KnotConsts kc(K);
   const int nq = op_end - op_begin;
@@ -216,23 +315,25 @@ __global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
     if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
       rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
-      shift_bounds_op<INV>(blob + op.sb, xs, s, hh, rot, D, ld);
+      shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
       floatx16 hb[kX3T];
-      layer0<kX3T>(op, blob, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
-      // Hidden layers 1..n_hidden-1 (:343-345), two groups each.
+      X3_MARK(3);
+      layer0<kX3T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
+      X3_MARK(4);
+      // Hidden layers 1..n_hidden-1 (:343-345), kX3T / GT groups each.
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[kX3T];
 #pragma unroll
         for (int o = 0; o < kX3T; ++o) acc[o] = floatx16{0};
-        x3_step<kX3T, 0, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, acc, wave, lane);
-        x3_step<kX3T, 1, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, acc, wave, lane);
+        x3_layer<NL, GT, NBUF, kX3T, INV>(F, x3, pipe, hb, acc, lane);
+        X3_MARK(5);
 #pragma unroll
         for (int o = 0; o < kX3T; ++o) {
           floatx4 bv[4];
-          bias_tile(blob + op.b[l] + o * 32, hh, bv);
+          bias_tile(sp + op.b[l] + o * 32, hh, bv);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r] + bv[r >> 2][r & 3]);
+          for (int r = 0; r < 16; ++r) hb[o][r] = (ZF_X3_ABLATE & 2) ? acc[o][r] + bv[r >> 2][r & 3] : swish(acc[o][r] + bv[r >> 2][r & 3]);
         }
       }
       // Last Dense (:346-347): lane half h, tile o, register r = parameter
@@ -240,53 +341,62 @@ __global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
       floatx16 pa[TL];
 #pragma unroll
       for (int o = 0; o < TL; ++o) pa[o] = floatx16{0};
-      x3_step<TL, 0, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, pa, wave, lane);
-      x3_step<TL, 1, INV>(F, x3, cur, op_begin, op_end, wbuf, buf, hb, pa, wave, lane);
+      X3_MARK(6);
+      x3_layer<NL, GT, NBUF, TL, INV>(F, x3, pipe, hb, pa, lane);
+      X3_MARK(7);
       float P[TL * 16];
 #pragma unroll
       for (int o = 0; o < TL; ++o) {
         floatx4 bv[4];
-        bias_tile(blob + op.x3_blast + o * 32, hh, bv);
+        bias_tile(sp + op.x3_blast + o * 32, hh, bv);
 #pragma unroll
         for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r] + bv[r >> 2][r & 3];
       }
       // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
       const int dt = op.dt;
       float ldv = 0.f;
-      if (hh < dt) {
+      const bool act = hh < dt;  // lane half h transforms dim h (idle half when dt == 1)
+      {
         float w[K], hg[K];
         float sx = 0.f, sy = 0.f;
 #pragma unroll
         for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-          w[j] = squareplus_fast(P[j]);
-          hg[j] = squareplus_fast(P[K + j]);
+          w[j] = squareplus_rsq(P[j]);
+          hg[j] = squareplus_rsq(P[K + j]);
           sx = sx + w[j];
           sy = sy + hg[j];
         }
-        const float rsx = rcp_refined(sx), rsy = rcp_refined(sy);
+        // (v / sum + c) / (1 + c K) as one fma per knot: the parameters
+        // themselves already differ from the reference's in the last ulp
+        // (GEMM summation order), so correctly rounded divisions buy nothing.
+        const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
+        const float bc = kc.c * kc.rnorm;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          w[j] = div_cr(div_cr(w[j], sx, rsx) + kc.c, kc.norm, kc.rnorm);
-          hg[j] = div_cr(div_cr(hg[j], sy, rsy) + kc.c, kc.norm, kc.rnorm);
+          w[j] = __builtin_fmaf(w[j], ax, bc);
+          hg[j] = __builtin_fmaf(hg[j], ay, bc);
         }
         auto slope = [&](int j) {  // derivative at inner knot j+1 (j in [0, K-2])
           float v = P[2 * K];
 #pragma unroll
           for (int jj = 1; jj < K - 1; ++jj) v = (j == jj) ? P[2 * K + jj] : v;
-          return squareplus_fast(v);
+          return squareplus_rsq(v);
         };
         float* xp = xs + pmod(hh + rot, D) * 32 + s;
         const float xv = *xp;
         const RqsBin bin = rqs_bin_regs<!INV, K>(xv, w, hg, slope);
+        float yv;
         if (!INV) {
-          float yv;
-          rqs_forward_eval(xv, bin, yv, ldv);
-          *xp = yv;
+          float l;
+          rqs_forward_eval(xv, bin, yv, l);
+          ldv = act ? l : 0.f;
         } else {
-          *xp = rqs_inverse_eval(xv, bin);
+          yv = rqs_inverse_eval(xv, bin);
         }
+        if (act) *xp = yv;
       }
       wave_lds_sync();
+      X3_MARK(8);
       if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139), Chain += (bijectors.py:110)
         const float other = __shfl_xor(ldv, 32);
         float ldc = hh == 0 ? ldv : other;
@@ -296,8 +406,11 @@ __global__ __launch_bounds__(kX3Rows * 2, 1) void flow_kernel_x3(
     }
   }
 
-  flow_epilogue<kX3Waves>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial,
-                          kX3Rows / 128, nparts, y_out, ld_out, s_part);
+  if (PIPE && pipe.lead >= 0) __syncthreads();  // leading half: matching trailing step
+  X3_MARK(9);
+  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial,
+                    NW * kTile / 128, nparts, y_out, ld_out, s_part);
+  X3_MARK(10);
 }
 
 uint16_t bf16_rne(float f) {
@@ -340,7 +453,7 @@ int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
 // Pack the group streams (bf16 hi/mid/lo A fragments) of every NSC and the
 // row-permuted last-layer biases (into `packed` at F.ops[i].x3_blast, which
 // the caller allocated with x3_last_tiles(K)*32 floats).
-void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* packed,
+void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream) {
   stream.clear();
   int prev = -1;
@@ -358,21 +471,21 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* pack
     const int TL = x3_last_tiles(K);
     d.x3 = (long long)stream.size() * 2;
     d.x3_tlast = TL;
-    d.x3_groups = 2 * op.n_hidden;
+    d.x3_groups = (kX3T / GT) * op.n_hidden;
     for (int l = 1; l <= op.n_hidden; ++l) {
       const bool last = (l == op.n_hidden);
       const int in = op.hidden[l - 1];
       const int out = last ? dt * S : op.hidden[l];
       const int NOUT = last ? TL : kX3T;
       const float* W = nat + op.off_w[l];
-      for (int q = 0; q < 2; ++q)
-        for (int tl = 0; tl < 2; ++tl)
+      for (int q = 0; q < kX3T / GT; ++q)
+        for (int tl = 0; tl < GT; ++tl)
           for (int s = 0; s < 2; ++s)
             for (int o = 0; o < NOUT; ++o) {
               uint16_t part[3][64][8];
               for (int ln = 0; ln < 64; ++ln)
                 for (int j = 0; j < 8; ++j) {
-                  const int kstep = 2 * (2 * q + tl) + s;
+                  const int kstep = 2 * (GT * q + tl) + s;
                   const int k = 16 * kstep + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3);
                   const int rho = ln & 31;
                   int col;
@@ -407,29 +520,66 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, DevFlow& F, float* pack
   }
 }
 
-size_t x3_lds_bytes(int D) {
-  return (size_t)2 * kX3Buf + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
+template <int NW, int GT, int PIPE>
+size_t lds_bytes(int small_floats, int D) {
+  return (size_t)(PIPE ? 3 : 2) * group_bytes(GT, kX3T) + (size_t)((small_floats + 3) & ~3) * 4 +
+         (size_t)NW * 32 * D * 4 + NW * sizeof(double);
 }
 
-int launch_flow_x3(const X3Launch& a, bool inverse) {
-  const long long grid = (a.N + kX3Rows - 1) / kX3Rows;
+template <int K, int NW, int GT, int PIPE>
+int launch_x3(const X3Launch& a, bool inverse) {
+  const long long rows = NW * kTile;
+  const long long grid = (a.N + rows - 1) / rows;
   if (grid > 0x7fffffffLL) return einval("N too large");
-  const size_t lds = x3_lds_bytes(a.D);
+  const size_t lds = lds_bytes<NW, GT, PIPE>(a.small_floats, a.D);
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
-#define ZF_X3(KV, IV)                                                                                 \
-  hipLaunchKernelGGL((flow_kernel_x3<KV, IV>), dim3((unsigned)grid), dim3(kX3Rows * 2), lds, a.stream, \
-                     a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,    \
-                     a.nparts, a.op_begin, a.op_end, a.N)
-  if (a.K == 16) {
-    if (inverse) ZF_X3(16, true); else ZF_X3(16, false);
-  } else if (a.K == 8) {
-    if (inverse) ZF_X3(8, true); else ZF_X3(8, false);
-  } else {
-    return enotsup("bf16x3 kernel: knots must be 8 or 16");
-  }
-#undef ZF_X3
+  if (inverse)
+    hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, true>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
+                       a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
+                       a.nparts, a.op_begin, a.op_end, a.N);
+  else
+    hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, false>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
+                       a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
+                       a.nparts, a.op_begin, a.op_end, a.N);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
   return ZF_OK;
 }
+
+template <int K>
+int launch_x3_k(const X3Launch& a, bool inverse) {
+  switch (a.variant) {
+    case 1: return launch_x3<K, 4, 1, 0>(a, inverse);  // 4 waves, 1-tile groups, 2 blocks per CU
+    case 2: return launch_x3<K, 8, 2, 1>(a, inverse);  // 8 waves, half-blocks offset by one group
+    case 3: return launch_x3<K, 8, 1, 1>(a, inverse);  // same with 1-tile groups
+    default: return launch_x3<K, 8, 2, 0>(a, inverse); // 8 waves in lockstep
+  }
+}
+
+int launch_flow_x3(const X3Launch& a, bool inverse) {
+  if (a.K == 16) return launch_x3_k<16>(a, inverse);
+  if (a.K == 8) return launch_x3_k<8>(a, inverse);
+  return enotsup("bf16x3 kernel: knots must be 8 or 16");
+}
+
+#if ZF_X3_TRACE
+extern "C" int zf_debug_x3_trace(unsigned long long* out, int* counts) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_trace), sizeof(g_x3_trace));
+  (void)hipMemcpyFromSymbol(counts, HIP_SYMBOL(g_x3_trace_n), sizeof(g_x3_trace_n));
+  int z[32] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_x3_trace_n), z, sizeof(z));
+  return 0;
+}
+#endif
+
+size_t x3_lds_bytes(int variant, int small_floats, int D) {
+  switch (variant) {
+    case 1: return lds_bytes<4, 1, 0>(small_floats, D);
+    case 2: return lds_bytes<8, 2, 1>(small_floats, D);
+    case 3: return lds_bytes<8, 1, 1>(small_floats, D);
+    default: return lds_bytes<8, 2, 0>(small_floats, D);
+  }
+}
+
+int x3_group_tiles(int variant) { return (variant == 1 || variant == 3) ? 1 : 2; }
 
 }  // namespace zf
