@@ -5,7 +5,9 @@ known-answer tests).  Run: ``python tests/golden/make_golden.py``.
 * rqs_K{8,16,32}.npz — utils.rational_quadratic_spline_{forward,inverse}
   inputs/outputs (M=2048, N=2, logits with sigma in {0.1, 1, 3}, x incl. OOB);
 * flow_<cfg>.npz — Flow.log_prob for BASELINE configs at small N, with the
-  case metadata (inputs are regenerated from the seed and checked equal).
+  case metadata (inputs are regenerated from the seed and checked equal);
+* flow_cfg3_inverse.npz — config 3 (the cfg2 flow run backwards, Chain.inverse
+  as in Flow.sample): z = 0.5 + 0.1 N(0, 1) -> x, fp32 and fp64 oracle.
 """
 
 import json
@@ -49,8 +51,19 @@ def flow_fixtures():
                             sensitivity=sens, meta=np.array(meta))
 
 
+def inverse_fixture():
+    name, N, seed = "cfg2", 1024, 103
+    case = make_case(name, N=N, seed=seed)
+    z = (0.5 + 0.1 * np.random.default_rng(4).standard_normal((N, 4))).astype(np.float32)
+    x = O.flow_inverse(case["model"], case["variables"], z, None)
+    x64 = O.flow_inverse(case["model"], case["variables"], z.astype(np.float64), None, dtype=np.float64)
+    meta = json.dumps({"name": name, "N": N, "seed": seed, "z_seed": 4})
+    np.savez_compressed(OUT / "flow_cfg3_inverse.npz", z=z, x=x, x64=x64, meta=np.array(meta))
+
+
 if __name__ == "__main__":
     rqs_fixtures()
     flow_fixtures()
+    inverse_fixture()
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

@@ -1,0 +1,48 @@
+"""The committed golden fixtures (tests/golden/make_golden.py) are reproduced
+by the CPU oracle: inputs regenerate bit-identically from their seeds and the
+oracle's outputs match the stored ones (BLAS summation order may differ
+between hosts, hence a 1e-6 relative tolerance on the MLP-dependent values)."""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+from numpy.testing import assert_allclose
+
+from oracle import zf_oracle as O
+from tests.flowcases import make_case
+
+G = Path(__file__).parent / "golden"
+
+
+@pytest.mark.parametrize("K", [8, 16, 32])
+def test_rqs_fixture(K):
+    d = np.load(G / f"rqs_K{K}.npz")
+    y, ld = O.rqs_forward(d["x"], d["dx"], d["dy"], d["slope"])
+    assert np.array_equal(y, d["y"], equal_nan=True)
+    assert np.array_equal(ld, d["log_det"], equal_nan=True)
+    xi = O.rqs_inverse(d["y"], d["dx"], d["dy"], d["slope"])
+    assert np.array_equal(xi, d["x_inv"], equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg5"])
+def test_flow_fixture(name):
+    d = np.load(G / f"flow_{name}.npz")
+    meta = json.loads(str(d["meta"]))
+    case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
+    assert np.array_equal(case["x"], d["x"])
+    lp, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"])
+    fin = np.isfinite(d["log_prob"])
+    assert np.array_equal(np.isfinite(lp), fin)
+    assert_allclose(lp[fin], d["log_prob"][fin], rtol=1e-6, atol=1e-6)
+
+
+def test_inverse_fixture():
+    d = np.load(G / "flow_cfg3_inverse.npz")
+    meta = json.loads(str(d["meta"]))
+    case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
+    z = (0.5 + 0.1 * np.random.default_rng(int(meta["z_seed"])).standard_normal((int(meta["N"]), 4)))
+    assert np.array_equal(z.astype(np.float32), d["z"])
+    x = O.flow_inverse(case["model"], case["variables"], d["z"], None)
+    assert_allclose(x, d["x"], rtol=1e-6, atol=1e-6)

@@ -97,7 +97,7 @@ def test_golden_flows():
     from pathlib import Path
 
     g = Path(__file__).parent / "golden"
-    for f in sorted(g.glob("flow_*.npz")):
+    for f in sorted(g.glob("flow_cfg?.npz")):
         d = np.load(f)
         meta = json.loads(str(d["meta"]))
         case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
@@ -108,6 +108,25 @@ def test_golden_flows():
         assert np.mean(np.isfinite(ref) != np.isfinite(lp)) <= 1e-3
         allow = REL * np.maximum(1.0, np.abs(ref64[fin])) + 2 * (np.abs(ref[fin] - ref64[fin]) + sens[fin])
         assert np.all(np.abs(lp[fin].astype(np.float64) - ref64[fin]) <= allow), f.name
+
+
+def test_golden_inverse_cfg3():
+    """Config 3 (Flow.sample's Chain.inverse on a given z) against the committed
+    fp32/fp64 oracle fixture: |gpu - x64| <= 1e-5 (1 + |x64|) + 2 |x32 - x64|."""
+    import json
+    from pathlib import Path
+
+    d = np.load(Path(__file__).parent / "golden" / "flow_cfg3_inverse.npz")
+    meta = json.loads(str(d["meta"]))
+    case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
+    flow = build_flow(case["cfg"])
+    sub = {k: v["bijector"] for k, v in case["variables"].items()}
+    x = flow.bijector.apply(sub, d["z"], None, method="inverse")
+    x32, x64 = d["x"], d["x64"]
+    fin = np.isfinite(x) & np.isfinite(x64)
+    assert fin.mean() > 0.999
+    allow = REL * (1 + np.abs(x64[fin])) + 2 * np.abs(x32[fin] - x64[fin])
+    assert np.all(np.abs(x[fin] - x64[fin]) <= allow)
 
 
 # --- full-size (batch 2^20) size-independent properties ---------------------------

@@ -46,9 +46,6 @@ constexpr int kX3T = 4;  // hidden tiles (hidden padded to 128)
 // Bytes of one weight group covering GT input tiles: [tl][s][o][part] x 1 KiB.
 constexpr int group_bytes(int GT, int NOUT) { return GT * 2 * NOUT * 3 * 1024; }
 
-#ifndef ZF_X3_ABLATE
-#define ZF_X3_ABLATE 0
-#endif
 #ifndef ZF_X3_TRACE
 #define ZF_X3_TRACE 0
 #endif
@@ -81,12 +78,6 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
   for (int i = 0; i < 4; ++i) {
     const floatx2 x = {v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
     const bf16x2 h = __builtin_convertvector(x, bf16x2);
-#if ZF_X3_ABLATE & 4
-    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
-    bm[2 * i] = h[0]; bm[2 * i + 1] = h[1];
-    bl[2 * i] = h[0]; bl[2 * i + 1] = h[1];
-    continue;
-#endif
     const floatx2 r = x - __builtin_convertvector(h, floatx2);
     const bf16x2 m = __builtin_convertvector(r, bf16x2);
     const floatx2 r2 = r - __builtin_convertvector(m, floatx2);
@@ -100,11 +91,6 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
                                           floatx16 acc) {
-#if ZF_X3_ABLATE & 8
-  asm volatile("" ::"v"(ah), "v"(am), "v"(al), "v"(bh), "v"(bm), "v"(bl));
-  acc[0] += 1.0f;
-  return acc;
-#endif
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
@@ -139,23 +125,40 @@ __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[k
   }
 }
 
-// Group stream cursor: the group most recently issued (op index + group).
-struct X3Cursor {
-  int op, g;
+// The group stream of the NSC being computed (byte offsets into the x3
+// blob), set up at NSC entry from the op's scalar fields: the per-step
+// prefetch then needs no memory access of its own (a scalar load there would
+// make its lgkmcnt wait drain the step's LDS reads too).
+struct X3Span {
+  long long base;       // group 0 of this NSC
+  long long next_base;  // group 0 of the next NSC in execution order within range, or -1
+  int G, nhid;          // groups in this NSC, hidden-layer groups among them
+  int last_pieces;      // KiB pieces of one last-layer group
+  int next_pieces;      // KiB pieces of the next NSC's group 0
 };
 
 template <int GT>
-__device__ __forceinline__ void group_span(const DevOp& op, int g, long long& off, int& pieces) {
-  constexpr int per_layer = kX3T / GT;
-  const int nhid = per_layer * (op.n_hidden - 1);
-  if (g < nhid) {
-    off = op.x3 + (long long)g * group_bytes(GT, kX3T);
-    pieces = group_bytes(GT, kX3T) >> 10;
+__device__ __forceinline__ int first_pieces(const DevOp& op) {
+  return (op.n_hidden > 1 ? group_bytes(GT, kX3T) : group_bytes(GT, op.x3_tlast)) >> 10;
+}
+
+template <int GT, bool INV>
+__device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int oi, int op_begin, int op_end) {
+  const DevOp& op = F->ops[oi];
+  X3Span sp;
+  sp.base = op.x3;
+  sp.G = op.x3_groups;
+  sp.nhid = (kX3T / GT) * (op.n_hidden - 1);
+  sp.last_pieces = group_bytes(GT, op.x3_tlast) >> 10;
+  const int n = op.x3_next[INV ? 1 : 0];
+  if (n >= op_begin && n < op_end) {
+    sp.next_base = F->ops[n].x3;
+    sp.next_pieces = first_pieces<GT>(F->ops[n]);
   } else {
-    const int lb = group_bytes(GT, op.x3_tlast);
-    off = op.x3 + (long long)nhid * group_bytes(GT, kX3T) + (long long)(g - nhid) * lb;
-    pieces = lb >> 10;
+    sp.next_base = -1;
+    sp.next_pieces = 0;
   }
+  return sp;
 }
 
 // Issue the DMA of one group into an LDS buffer: 1 KiB pieces (one
@@ -164,7 +167,6 @@ __device__ __forceinline__ void group_span(const DevOp& op, int g, long long& of
 template <int NW>
 __device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave,
                                        int lane) {
-  if (ZF_X3_ABLATE & 16) return;
   for (int p = wave; p < pieces; p += NW)
     __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
                                      (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
@@ -172,40 +174,41 @@ __device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, 
 
 // Block-wide weight-group pipeline state (every field wave-uniform).
 struct X3Pipe {
-  char* wbuf;      // [NBUF][group bytes] LDS ring
-  int buf;         // ring slot holding the group this wave computes next
-  X3Cursor cur;    // group most recently issued (DMA-issuing waves only)
-  int op_begin, op_end;
-  int lead;        // index of this wave among the NL DMA-issuing waves, or -1
+  char* wbuf;   // [NBUF][group bytes] LDS ring
+  int buf;      // ring slot holding the group this wave computes next
+  int g;        // index of that group within the current NSC
+  X3Span span;  // current NSC's group stream
+  int lead;     // index of this wave among the NL DMA-issuing waves, or -1
 };
 
-// Advance the cursor to the next group in execution order within
-// [op_begin, op_end) and DMA it into `dst`; no-op at the end of the stream.
-template <int NL, int GT, bool INV>
-__device__ __forceinline__ void x3_issue_next(const DevFlow* __restrict__ F, const char* __restrict__ x3,
-                                              X3Pipe& p, char* dst, int lane) {
-  if (p.cur.op < 0) return;
-  int op = p.cur.op, g = p.cur.g + 1;
-  if (g >= F->ops[op].x3_groups) {
-    op = F->ops[op].x3_next[INV ? 1 : 0];
-    g = 0;
-    if (op < p.op_begin || op >= p.op_end) op = -1;
-  }
-  p.cur.op = op;
-  p.cur.g = g;
-  if (op < 0) return;
+// DMA the group after group p.g (the next one of this NSC, or group 0 of
+// the next NSC) into `dst`; nothing at the end of the stream.
+template <int NL, int GT>
+__device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
+  constexpr int kHid = group_bytes(GT, kX3T);
+  const int g = p.g + 1;
   long long off;
   int pieces;
-  group_span<GT>(F->ops[op], g, off, pieces);
+  if (g < p.span.nhid) {
+    off = p.span.base + (long long)g * kHid;
+    pieces = kHid >> 10;
+  } else if (g < p.span.G) {
+    off = p.span.base + (long long)p.span.nhid * kHid + (long long)(g - p.span.nhid) * (p.span.last_pieces << 10);
+    pieces = p.span.last_pieces;
+  } else {
+    if (p.span.next_base < 0) return;
+    off = p.span.next_base;
+    pieces = p.span.next_pieces;
+  }
   x3_dma<NL>(x3 + off, dst, pieces, p.lead, lane);
 }
 
 // One pipeline step: wait for this wave's DMAs, block barrier (the group in
 // slot `buf` is complete and the slot after it is free), the issuing waves
 // prefetch the next group into the next slot, then this group's MFMAs.
-template <int NL, int GT, int NBUF, int NOUT, int Q, bool INV>
-__device__ __forceinline__ void x3_step(const DevFlow* __restrict__ F, const char* __restrict__ x3, X3Pipe& p,
-                                        const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int lane) {
+template <int NL, int GT, int NBUF, int NOUT, int Q>
+__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
+                                        floatx16 (&acc)[NOUT], int lane) {
   constexpr int kBuf = group_bytes(GT, kX3T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -219,17 +222,18 @@ __device__ __forceinline__ void x3_step(const DevFlow* __restrict__ F, const cha
     else __builtin_amdgcn_s_setprio(0);
   }
   const int nb = (p.buf + 1 == NBUF) ? 0 : p.buf + 1;
-  if (p.lead >= 0) x3_issue_next<NL, GT, INV>(F, x3, p, p.wbuf + nb * kBuf, lane);
+  if (p.lead >= 0) x3_issue_next<NL, GT>(x3, p, p.wbuf + nb * kBuf, lane);
   x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
   p.buf = nb;
+  p.g += 1;
 }
 
 // A whole streamed Dense layer: kX3T / GT groups.
-template <int NL, int GT, int NBUF, int NOUT, bool INV, int Q = 0>
-__device__ __forceinline__ void x3_layer(const DevFlow* __restrict__ F, const char* __restrict__ x3, X3Pipe& p,
-                                         const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT], int lane) {
-  x3_step<NL, GT, NBUF, NOUT, Q, INV>(F, x3, p, hb, acc, lane);
-  if constexpr (Q + 1 < kX3T / GT) x3_layer<NL, GT, NBUF, NOUT, INV, Q + 1>(F, x3, p, hb, acc, lane);
+template <int NL, int GT, int NBUF, int NOUT, int Q = 0>
+__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
+                                         floatx16 (&acc)[NOUT], int lane) {
+  x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane);
+  if constexpr (Q + 1 < kX3T / GT) x3_layer<NL, GT, NBUF, NOUT, Q + 1>(x3, p, hb, acc, lane);
 }
 
 // squareplus with a Newton-corrected reciprocal square root (one
@@ -287,22 +291,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
   X3Pipe pipe;
   pipe.wbuf = lds;
   pipe.buf = 0;
-  pipe.cur = X3Cursor{-1, 0};
-  pipe.op_begin = op_begin;
-  pipe.op_end = op_end;
+  pipe.g = 0;
   pipe.lead = wave < NL ? wave : -1;
-  {  // first group of the first NSC in execution order goes out now
+  {  // group 0 of the first NSC in execution order goes out now
+    int first = -1;
     const int nq = op_end - op_begin;
     for (int q = 0; q < nq; ++q) {
       const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
-      if (F->ops[oi].kind == ZF_OP_NSC) { pipe.cur.op = oi; break; }
+      if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
     }
-    if (pipe.cur.op >= 0 && pipe.lead >= 0) {
-      long long off;
-      int pieces;
-      group_span<GT>(F->ops[pipe.cur.op], 0, off, pieces);
-      x3_dma<NL>(x3 + off, pipe.wbuf, pieces, pipe.lead, lane);
-    }
+    if (first >= 0 && pipe.lead >= 0)
+      x3_dma<NL>(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<GT>(F->ops[first]), pipe.lead, lane);
   }
   if (PIPE && pipe.lead < 0) __syncthreads();  // trailing half starts one step late
 
@@ -317,6 +316,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
       shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
+      pipe.span = make_span<GT, INV>(F, oi, op_begin, op_end);
+      pipe.g = 0;
       floatx16 hb[kX3T];
       X3_MARK(3);
       layer0<kX3T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
@@ -326,14 +327,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
         floatx16 acc[kX3T];
 #pragma unroll
         for (int o = 0; o < kX3T; ++o) acc[o] = floatx16{0};
-        x3_layer<NL, GT, NBUF, kX3T, INV>(F, x3, pipe, hb, acc, lane);
+        x3_layer<NL, GT, NBUF, kX3T>(x3, pipe, hb, acc, lane);
         X3_MARK(5);
 #pragma unroll
         for (int o = 0; o < kX3T; ++o) {
           floatx4 bv[4];
           bias_tile(sp + op.b[l] + o * 32, hh, bv);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hb[o][r] = (ZF_X3_ABLATE & 2) ? acc[o][r] + bv[r >> 2][r & 3] : swish(acc[o][r] + bv[r >> 2][r & 3]);
+          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r] + bv[r >> 2][r & 3]);
         }
       }
       // Last Dense (:346-347): lane half h, tile o, register r = parameter
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
 #pragma unroll
       for (int o = 0; o < TL; ++o) pa[o] = floatx16{0};
       X3_MARK(6);
-      x3_layer<NL, GT, NBUF, TL, INV>(F, x3, pipe, hb, pa, lane);
+      x3_layer<NL, GT, NBUF, TL>(x3, pipe, hb, pa, lane);
       X3_MARK(7);
       float P[TL * 16];
 #pragma unroll
@@ -376,15 +377,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
           w[j] = __builtin_fmaf(w[j], ax, bc);
           hg[j] = __builtin_fmaf(hg[j], ay, bc);
         }
-        auto slope = [&](int j) {  // derivative at inner knot j+1 (j in [0, K-2])
-          float v = P[2 * K];
+        float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
-          for (int jj = 1; jj < K - 1; ++jj) v = (j == jj) ? P[2 * K + jj] : v;
-          return squareplus_rsq(v);
-        };
+        for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
         float* xp = xs + pmod(hh + rot, D) * 32 + s;
         const float xv = *xp;
-        const RqsBin bin = rqs_bin_regs<!INV, K>(xv, w, hg, slope);
+        const RqsBin bin = rqs_bin_regs_sl<!INV, K>(xv, w, hg, sl, [](float v) { return squareplus_rsq(v); });
         float yv;
         if (!INV) {
           float l;

@@ -108,6 +108,60 @@ __device__ __forceinline__ RqsBin rqs_bin_regs(float v, const float (&w)[K], con
   return b;
 }
 
+// rqs_bin_regs with the K-1 inner-knot slope inputs also in registers: the
+// two the bin needs are picked by the same sweep (static register indices
+// only: a dynamic index into a register array would go through scratch),
+// then mapped by `tf` (squareplus for raw conditioner logits, identity for
+// slopes).  Same count / fill-mode semantics as rqs_bin.
+template <bool FWD, int K, class TF>
+__device__ __forceinline__ RqsBin rqs_bin_regs_sl(float v, const float (&w)[K], const float (&h)[K],
+                                                  const float (&sl)[K - 1], const TF& tf) {
+  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  float lo = 0.f, hi = (K > 1) ? sl[0] : 0.f;  // raw slope inputs at knots sel, sel+1
+  int cnt = 0, sel = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) {
+      ++cnt; sel = j; sxk = xk; syk = yk; sw = w[j]; sh = h[j];
+      if (j >= 1) lo = sl[j - 1];
+      if (j + 1 < K) hi = sl[j];
+    }
+    xk = xk + w[j];
+    yk = yk + h[j];
+  }
+  {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; sw = qnan(); sh = qnan(); }
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  if (idx != sel) {  // non-monotone knots (never from normalize_spline_params)
+    xk = 0.f; yk = 0.f;
+    sw = qnan(); sh = qnan();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j == idx) {
+        sw = w[j]; sh = h[j];
+        if (j >= 1) lo = sl[j - 1];
+        if (j + 1 < K) hi = sl[j];
+      }
+      if (j < idx) { xk = xk + w[j]; yk = yk + h[j]; }
+    }
+    sxk = xk; syk = yk; sel = idx;
+  }
+  RqsBin b;
+  b.xk = sxk;
+  b.yk = syk;
+  b.w = sw;
+  b.h = sh;
+  b.dk = (sel == 0 || sel == K) ? 1.0f : tf(lo);
+  b.dkp1 = (sel + 1 < K) ? tf(hi) : (sel + 1 == K ? 1.0f : qnan());
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+
 // utils.py:121-139 — forward value and per-dim log|dy/dx|.
 __device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
   const float zr = (x - b.xk) / b.w;               // :122
