@@ -46,13 +46,14 @@ names = {0: "start", 1: "arrive", 2: "depart", 3: "nsc", 4: "l0_done", 5: "hid_d
          7: "last_done", 8: "spline_done", 9: "ops_done", 10: "end"}
 for tb in range(4):
     tot = defaultdict(float)
-    for w in range(8):
+    waves = [w for w in range(8) if n[tb, w] > 0]
+    for w in waves:
         k = min(int(n[tb, w]), 256)
         ev = (a[tb, w, :k] >> 48).astype(int)
         t = (a[tb, w, :k] & ((1 << 48) - 1)).astype(np.int64)
         t = t - t[0]
         for i in range(1, k):
-            tot[(names[ev[i - 1]], names[ev[i]])] += (t[i] - t[i - 1]) / 8
+            tot[(names[ev[i - 1]], names[ev[i]])] += (t[i] - t[i - 1]) / len(waves)
     span = sum(tot.values())
     print(f"block#{tb}: avg wave span {span:.0f} ticks; segments (avg per wave, ticks):")
     for key, val in sorted(tot.items(), key=lambda kv: -kv[1]):

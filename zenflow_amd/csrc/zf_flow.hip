@@ -574,9 +574,9 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   std::vector<uint16_t> x3s;
   if (x3) {
     const char* v = std::getenv("ZF_X3_VARIANT");
-    // default: 4-wave blocks, one-tile groups, two blocks per CU (zf_flow_x3.hip)
-    h->x3_variant = (v && v[0] >= '0' && v[0] <= '3') ? v[0] - '0' : 1;
-    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) > 160 * 1024) h->x3_variant = 1;
+    // default: 4-wave blocks, one-tile groups, three blocks per CU (zf_flow_x3.hip)
+    h->x3_variant = (v && v[0] >= '0' && v[0] <= '4') ? v[0] - '0' : 4;
+    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) > 160 * 1024) h->x3_variant = 4;
     if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) <= 160 * 1024) {
       zf::x3_pack(desc, nat, zf::x3_group_tiles(h->x3_variant), F, P, x3s);
       F.x3_ok = 1;

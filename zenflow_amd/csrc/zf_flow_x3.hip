@@ -251,9 +251,11 @@ __device__ __forceinline__ float squareplus_rsq(float x) {
 // group — waves [0, NW/2) issue every DMA and compute group t while waves
 // [NW/2, NW) compute group t-1 (NBUF = 3) — so one half's VALU phases
 // (spline, swish epilogues, layer 0) overlap the other half's MFMAs on the
-// same SIMD.
+// same SIMD.  PIPE 2: lockstep, small parameters read from global memory
+// (L2-resident) instead of LDS, so that three 4-wave blocks fit a CU's LDS
+// (3 waves per SIMD, <= 168 VGPRs).
 template <int K, int NW, int GT, int PIPE, bool INV>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
+__global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
@@ -267,20 +269,22 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
   const int s = lane & 31;
   const int hh = lane >> 5;
   constexpr int kBuf = group_bytes(GT, kX3T);
-  constexpr int NBUF = PIPE ? 3 : 2;
-  constexpr int NL = PIPE ? NW / 2 : NW;  // DMA-issuing waves
+  constexpr int NBUF = PIPE == 1 ? 3 : 2;
+  constexpr int NL = PIPE == 1 ? NW / 2 : NW;  // DMA-issuing waves
+  constexpr bool kSmallLds = PIPE != 2;
   // LDS: [NBUF][kBuf] weight ring | small parameters | [NW][D][32] state | [NW] partials
-  const int small4 = (F->small_floats + 3) & ~3;
-  float* sp = reinterpret_cast<float*>(lds + NBUF * kBuf);
-  float* xs = sp + small4 + wave * (32 * D);
-  double* s_part = reinterpret_cast<double*>(sp + small4 + NW * 32 * D);
+  const int small4 = kSmallLds ? (F->small_floats + 3) & ~3 : 0;
+  float* lsm = reinterpret_cast<float*>(lds + NBUF * kBuf);
+  const float* sp = kSmallLds ? lsm : blob;
+  float* xs = lsm + small4 + wave * (32 * D);
+  double* s_part = reinterpret_cast<double*>(lsm + small4 + NW * 32 * D);
   const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
   const bool valid = row < N;
 
   X3_MARK(0);
   {  // small parameters -> LDS (before any DMA is in flight)
     const floatx4* src = reinterpret_cast<const floatx4*>(blob);
-    floatx4* dst = reinterpret_cast<floatx4*>(sp);
+    floatx4* dst = reinterpret_cast<floatx4*>(lsm);
     for (int i = threadIdx.x; i < small4 / 4; i += NW * 64) dst[i] = src[i];
   }
   load_state(xs, xin, row, valid, D, s, hh);
@@ -303,7 +307,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
     if (first >= 0 && pipe.lead >= 0)
       x3_dma<NL>(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<GT>(F->ops[first]), pipe.lead, lane);
   }
-  if (PIPE && pipe.lead < 0) __syncthreads();  // trailing half starts one step late
+  if (PIPE == 1 && pipe.lead < 0) __syncthreads();  // trailing half starts one step late
 
   const KnotConsts kc(K);
   const int nq = op_end - op_begin;
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
       layer0<kX3T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
       X3_MARK(4);
       // Hidden layers 1..n_hidden-1 (:343-345), kX3T / GT groups each.
-      for (int l = 1; l < op.n_hidden; ++l) {
+      auto hidden = [&](int l) {
         floatx16 acc[kX3T];
 #pragma unroll
         for (int o = 0; o < kX3T; ++o) acc[o] = floatx16{0};
@@ -336,7 +340,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
 #pragma unroll
           for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r] + bv[r >> 2][r & 3]);
         }
-      }
+      };
+      for (int l = 1; l < op.n_hidden; ++l) hidden(l);
       // Last Dense (:346-347): lane half h, tile o, register r = parameter
       // 16*o + r of transformed dim h.
       floatx16 pa[TL];
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void flow_kernel_x3(
     }
   }
 
-  if (PIPE && pipe.lead >= 0) __syncthreads();  // leading half: matching trailing step
+  if (PIPE == 1 && pipe.lead >= 0) __syncthreads();  // leading half: matching trailing step
   X3_MARK(9);
   flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial,
                     NW * kTile / 128, nparts, y_out, ld_out, s_part);
@@ -520,7 +525,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, flo
 
 template <int NW, int GT, int PIPE>
 size_t lds_bytes(int small_floats, int D) {
-  return (size_t)(PIPE ? 3 : 2) * group_bytes(GT, kX3T) + (size_t)((small_floats + 3) & ~3) * 4 +
+  return (size_t)(PIPE == 1 ? 3 : 2) * group_bytes(GT, kX3T) + (size_t)(PIPE == 2 ? 0 : (small_floats + 3) & ~3) * 4 +
          (size_t)NW * 32 * D * 4 + NW * sizeof(double);
 }
 
@@ -549,6 +554,7 @@ int launch_x3_k(const X3Launch& a, bool inverse) {
     case 1: return launch_x3<K, 4, 1, 0>(a, inverse);  // 4 waves, 1-tile groups, 2 blocks per CU
     case 2: return launch_x3<K, 8, 2, 1>(a, inverse);  // 8 waves, half-blocks offset by one group
     case 3: return launch_x3<K, 8, 1, 1>(a, inverse);  // same with 1-tile groups
+    case 4: return launch_x3<K, 4, 1, 2>(a, inverse);  // 4 waves, 3 blocks per CU
     default: return launch_x3<K, 8, 2, 0>(a, inverse); // 8 waves in lockstep
   }
 }
@@ -574,10 +580,11 @@ size_t x3_lds_bytes(int variant, int small_floats, int D) {
     case 1: return lds_bytes<4, 1, 0>(small_floats, D);
     case 2: return lds_bytes<8, 2, 1>(small_floats, D);
     case 3: return lds_bytes<8, 1, 1>(small_floats, D);
+    case 4: return lds_bytes<4, 1, 2>(small_floats, D);
     default: return lds_bytes<8, 2, 0>(small_floats, D);
   }
 }
 
-int x3_group_tiles(int variant) { return (variant == 1 || variant == 3) ? 1 : 2; }
+int x3_group_tiles(int variant) { return (variant == 1 || variant == 3 || variant == 4) ? 1 : 2; }
 
 }  // namespace zf
