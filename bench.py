@@ -35,6 +35,7 @@ WORKLOADS = {
     # name: (D, C, K, layers, couplings, latent, mode)
     "cfg2": (4, 0, 16, (128, 128), 4, "normal", "log_prob"),
     "cfg3": (4, 0, 16, (128, 128), 4, "normal", "inverse"),
+    "cfg3s": (4, 0, 16, (128, 128), 4, "normal", "sample"),  # Flow.sample, latent drawn on device
     "cfg4": (2, 2, 16, (128, 128), 2, "beta", "log_prob"),
     "cfg5": (16, 0, 32, (256, 256), 8, "normal", "log_prob"),
 }
@@ -237,6 +238,12 @@ def main():
             L.check(lib.zf_flow_nll_reduce(ws.ptr, N, nll.ptr, L.stream()), "nll_reduce")
             if comm is not None:
                 comm.allreduce_sum_(nll)
+        elif mode == "sample":
+            if ev is not None:
+                ev[0].record()
+            prog.sample(N, 1234 + rank, cd, out=out)
+            if ev is not None:
+                ev[1].record()
         else:
             if ev is not None:
                 ev[0].record()

@@ -205,6 +205,20 @@ int zf_flow_forward(zf_flow_t* h, int op_begin, int op_end, const float* x, cons
 int zf_flow_inverse(zf_flow_t* h, int op_begin, int op_end, const float* z, const float* c,
                     float* x, int64_t N, void* stream);
 
+/* Replaces Flow.sample (flow.py:50-78) end to end: the latent draw
+ * (distributions.py:61-62 / 75-78 / 106-112 / 125-126) happens on the device
+ * in the inverse kernel's prologue — Philox4x32-10 keyed by `seed`, counter =
+ * (row, dim, stream), so x[row] depends only on (seed, row) — then the whole
+ * Chain.inverse runs in the same launch.  c (N,C) or NULL -> x (N,D).
+ * jax.random's threefry bits are not reproduced (parity is statistical). */
+int zf_flow_sample(zf_flow_t* h, uint64_t seed, const float* c, float* x, int64_t N, void* stream);
+
+/* Replaces Distribution.sample (distributions.py:61-62 Normal, :75-78
+ * TruncatedNormal, :106-112 Beta(param, param), :125-126 Uniform): z (N,D)
+ * drawn with the same counter-based generator as zf_flow_sample (same seed
+ * -> the same z that zf_flow_sample maps through the inverse). */
+int zf_latent_sample(int latent, double param, uint64_t seed, float* z, int64_t N, int D, void* stream);
+
 /* Replace one NSC op's BatchNorm statistics (mean[DC], var[DC]) — flax
  * BatchNorm with use_running_average=False normalises by batch statistics. */
 int zf_flow_set_bn_stats(zf_flow_t* h, int op, const float* mean, const float* var);

@@ -67,6 +67,8 @@ class ZfFlowDesc(C.Structure):
 _vp = C.c_void_p
 _i64 = C.c_int64
 _int = C.c_int
+_u64 = C.c_uint64
+_dbl = C.c_double
 
 # name -> (restype, argtypes); mirrors include/zenflow_amd.h one-to-one.
 SIGNATURES = {
@@ -106,6 +108,8 @@ SIGNATURES = {
     "zf_flow_nll_reduce": (_int, [_vp, _i64, _vp, _vp]),
     "zf_flow_forward": (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "zf_flow_inverse": (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _vp]),
+    "zf_flow_sample": (_int, [_vp, _u64, _vp, _vp, _i64, _vp]),
+    "zf_latent_sample": (_int, [_int, _dbl, _u64, _vp, _i64, _int, _vp]),
     "zf_flow_set_bn_stats": (_int, [_vp, _int, _vp, _vp]),
     "zf_flow_set_sb_stats": (_int, [_vp, _int, _vp, _vp]),
     "zf_colstats_workspace_bytes": (_i64, [_i64, _int]),

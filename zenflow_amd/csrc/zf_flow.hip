@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const float* __restrict__ xin,
     const float* __restrict__ cin, float* __restrict__ y_out, const float* __restrict__ ld_in,
     float* __restrict__ ld_out, float* __restrict__ lp_out, double* __restrict__ block_partial,
-    int op_begin, int op_end, long long N) {
+    int op_begin, int op_end, long long N, unsigned long long seed, int gen) {
   constexpr int T = HP / 32;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double s_part[kWaves];
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
   const long long row = ((long long)blockIdx.x * kWaves + wave) * kTile + s;
   const bool valid = row < N;
 
-  load_state(xs, xin, row, valid, D, s, hh);
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, gen);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;  // logical dim j is stored in column (j + rot) mod D
   wave_lds_sync();
@@ -258,6 +258,16 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
 
   flow_epilogue<kWaves>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, 0,
                         y_out, ld_out, s_part);
+}
+
+// Distribution.sample on the device: one thread per (row, dim).
+__global__ __launch_bounds__(256) void latent_sample_kernel(int latent, float param, unsigned long long seed,
+                                                            float* __restrict__ z, long long n, int D) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long row = i / D;
+  const int d = (int)(i - row * D);
+  z[i] = latent_draw(latent, param, seed, row, d);
 }
 
 // Deterministic fixed-order sum of per-block partials -> out[0].
@@ -467,6 +477,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       const double a = desc.latent_param;
       F.lat_c0 = (float)(-(std::lgamma(a) + std::lgamma(a) - std::lgamma(2.0 * a)));
       F.lat_c1 = (float)a - 1.0f;
+      F.lat_c3 = (float)a;  // peakness, for on-device sampling
     } else if (desc.latent == ZF_LATENT_TRUNCNORM) {
       // _log_gauss_mass(-5, 5) = log1p(-ndtr(-5) - ndtr(-5))
       const float nd = (float)(0.5 * std::erfc(5.0 / std::sqrt(2.0)));
@@ -630,12 +641,12 @@ namespace {
 template <bool INV>
 int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const float* c, float* y,
                 const float* ld_in, float* ld_out, float* lp, double* part, int64_t N,
-                void* stream) {
+                void* stream, unsigned long long seed = 0, int gen = 0) {
   if (!h) return einval("handle is NULL");
   if (N < 0) return einval("N < 0");
   if (op_begin < 0 || op_end > h->host.n_ops || op_begin > op_end) return einval("bad op range");
   if (N == 0) return ZF_OK;
-  if (!x) return einval("x is NULL");
+  if (!x && !gen) return einval("x is NULL");
   if (h->host.C > 0 && !c) return einval("flow is conditional (C=%d) but c is NULL", h->host.C);
   if (h->host.x3_ok) {
     X3Launch a;
@@ -644,6 +655,8 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
     a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.variant = h->x3_variant;
     a.small_floats = h->host.small_floats;
+    a.seed = seed;
+    a.gen = gen;
     a.stream = (hipStream_t)stream;
     return launch_flow_x3(a, INV);
   }
@@ -655,7 +668,7 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
   const long long n = (long long)N;
 #define ZF_LAUNCH(HPV)                                                                          \
   hipLaunchKernelGGL((flow_kernel<HPV, INV>), dim3((unsigned)grid), dim3(kWaves * 64), lds, st, \
-                     h->d_desc, h->d_blob, x, c, y, ld_in, ld_out, lp, part, op_begin, op_end, n)
+                     h->d_desc, h->d_blob, x, c, y, ld_in, ld_out, lp, part, op_begin, op_end, n, seed, gen)
   switch (h->host.HP) {
     case 32: ZF_LAUNCH(32); break;
     case 64: ZF_LAUNCH(64); break;
@@ -723,6 +736,29 @@ int zf_flow_inverse(zf_flow_t* h, int op_begin, int op_end, const float* z, cons
   if (!x && N > 0) return zf::einval("x is NULL");
   return zf::launch_flow<true>(h, op_begin, op_end, z, c, x, nullptr, nullptr, nullptr, nullptr,
                                N, stream);
+}
+
+int zf_flow_sample(zf_flow_t* h, uint64_t seed, const float* c, float* x, int64_t N, void* stream) {
+  if (!h) return zf::einval("handle is NULL");
+  if (!x && N > 0) return zf::einval("x is NULL");
+  if (h->host.latent == ZF_LATENT_NONE) return zf::einval("flow has no latent distribution");
+  return zf::launch_flow<true>(h, 0, h->host.n_ops, nullptr, c, x, nullptr, nullptr, nullptr, nullptr,
+                               N, stream, (unsigned long long)seed, 1);
+}
+
+int zf_latent_sample(int latent, double param, uint64_t seed, float* z, int64_t N, int D, void* stream) {
+  if (latent < ZF_LATENT_NORMAL || latent > ZF_LATENT_UNIFORM) return zf::einval("bad latent %d", latent);
+  if (latent == ZF_LATENT_BETA && !(param >= 1.0)) return zf::einval("Beta peakness must be >= 1");
+  if (N < 0 || D < 1) return zf::einval("bad shape");
+  if (N == 0) return ZF_OK;
+  if (!z) return zf::einval("z is NULL");
+  const long long n = (long long)N * D;
+  const long long grid = (n + 255) / 256;
+  if (grid > 0x7fffffffLL) return zf::einval("N too large");
+  hipLaunchKernelGGL(zf::latent_sample_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, latent,
+                     (float)param, (unsigned long long)seed, z, n, D);
+  ZF_CHECK_LAUNCH("latent_sample_kernel");
+  return ZF_OK;
 }
 
 static int upload_region(zf_flow* h, int64_t off, int64_t n) {

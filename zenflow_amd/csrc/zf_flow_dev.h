@@ -5,6 +5,7 @@
 // BatchNorm + first Dense layer, the latent log_prob epilogue).
 #pragma once
 #include "zf_internal.h"
+#include "zf_random.h"
 #include "zf_spline.h"
 
 #include <cstdint>
@@ -132,10 +133,16 @@ struct KnotConsts {
   }
 };
 
-// Per-wave state: xs[D][32] (column p = stored dim, lane = sample).
+// Per-wave state: xs[D][32] (column p = stored dim, lane = sample), from x
+// or — Flow.sample (flow.py:70-78) — drawn from the latent on the fly.
 __device__ __forceinline__ void load_state(float* xs, const float* __restrict__ xin, long long row,
-                                           bool valid, int D, int s, int hh) {
-  for (int d = hh; d < D; d += 2) xs[d * 32 + s] = valid ? xin[row * D + d] : 0.f;
+                                           bool valid, int D, int s, int hh, const DevFlow* __restrict__ F,
+                                           unsigned long long seed, int gen) {
+  for (int d = hh; d < D; d += 2) {
+    float v = 0.f;
+    if (valid) v = gen ? latent_draw(F->latent, F->lat_c3, seed, row, d) : xin[row * D + d];
+    xs[d * 32 + s] = v;
+  }
 }
 
 // ShiftBounds on the state (bijectors.py:181-208 forward, eval branch of
@@ -299,6 +306,8 @@ struct X3Launch {
   long long nparts;
   int op_begin, op_end;
   long long N;
+  unsigned long long seed;
+  int gen;  // 1: draw the input rows from the latent (zf_flow_sample)
   int K, D, variant, small_floats;
   hipStream_t stream;
 };

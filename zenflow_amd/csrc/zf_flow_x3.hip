@@ -259,7 +259,8 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
-    double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N) {
+    double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N,
+    unsigned long long seed, int gen) {
   constexpr int TL = (3 * K - 1 + 15) / 16;  // last-layer tiles: 16 parameters per lane half
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int D = F->D;
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
     floatx4* dst = reinterpret_cast<floatx4*>(lsm);
     for (int i = threadIdx.x; i < small4 / 4; i += NW * 64) dst[i] = src[i];
   }
-  load_state(xs, xin, row, valid, D, s, hh);
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, gen);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;
   __syncthreads();
@@ -539,11 +540,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
   if (inverse)
     hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, true>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
-                       a.nparts, a.op_begin, a.op_end, a.N);
+                       a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
     hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, false>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
-                       a.nparts, a.op_begin, a.op_end, a.N);
+                       a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
   return ZF_OK;
 }

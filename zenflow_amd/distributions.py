@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib as L
-from .random import as_generator
+from .random import key_to_seed
 
 
 class Distribution(ABC):
@@ -47,6 +47,20 @@ class Distribution(ABC):
     @abstractmethod
     def sample(self, nsamples: int, rngkey) -> np.ndarray: ...
 
+    def _device_sample(self, nsamples: int, rngkey) -> np.ndarray:
+        """Draw (nsamples, dim) on the GPU (zf_latent_sample: Philox keyed by
+        the key's 64-bit seed); the same z zf_flow_sample feeds the inverse."""
+        from .engine import _latent_code
+
+        if self.dim is None:
+            raise ValueError("dim unknown: call log_prob first")
+        code, param = _latent_code(self)
+        L.ensure_device()
+        z = L.DeviceArray((int(nsamples), self.dim))
+        L.check(L.load_library().zf_latent_sample(code, param, key_to_seed(rngkey), z.ptr, int(nsamples),
+                                                  self.dim, L.stream()), "zf_latent_sample")
+        return z.numpy()
+
     def __repr__(self):
         return f"{self.__class__.__name__}()"
 
@@ -55,21 +69,14 @@ class Normal(Distribution):
     """Multivariate normal, mean 0.5, standard deviation 0.1 (distributions.py:50-62)."""
 
     def sample(self, nsamples: int, rngkey) -> np.ndarray:
-        g = as_generator(rngkey)
-        return (0.5 + 0.1 * g.standard_normal((nsamples, self.dim))).astype(np.float32)
+        return self._device_sample(nsamples, rngkey)
 
 
 class TruncatedNormal(Distribution):
     """Normal truncated to [0, 1] (+-5 sigma) (distributions.py:65-78)."""
 
     def sample(self, nsamples: int, rngkey) -> np.ndarray:
-        g = as_generator(rngkey)
-        z = g.standard_normal((nsamples, self.dim))
-        bad = np.abs(z) > 5
-        while bad.any():
-            z[bad] = g.standard_normal(int(bad.sum()))
-            bad = np.abs(z) > 5
-        return (0.5 + 0.1 * z).astype(np.float32)
+        return self._device_sample(nsamples, rngkey)
 
 
 class Beta(Distribution):
@@ -82,8 +89,7 @@ class Beta(Distribution):
         self.peakness = peakness
 
     def sample(self, nsamples: int, rngkey) -> np.ndarray:
-        g = as_generator(rngkey)
-        return g.beta(self.peakness, self.peakness, (nsamples, self.dim)).astype(np.float32)
+        return self._device_sample(nsamples, rngkey)
 
     def __repr__(self):
         return f"{self.__class__.__name__}(peakness={self.peakness})"
@@ -93,5 +99,4 @@ class Uniform(Distribution):
     """Multivariate uniform on [0, 1] (distributions.py:119-126)."""
 
     def sample(self, nsamples: int, rngkey) -> np.ndarray:
-        g = as_generator(rngkey)
-        return g.uniform(size=(nsamples, self.dim)).astype(np.float32)
+        return self._device_sample(nsamples, rngkey)

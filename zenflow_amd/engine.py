@@ -223,6 +223,17 @@ class Program:
             "zf_flow_inverse")
         return x
 
+    def sample(self, N: int, seed: int, c=None, out=None):
+        """Flow.sample (flow.py:50-78) in one launch: latent drawn on the device
+        (Philox, zf_flow_sample), then Chain.inverse."""
+        if self.latent is None:
+            raise ValueError("flow has no latent distribution")
+        x = out if out is not None else DeviceArray((N, self.D))
+        check(L.load_library().zf_flow_sample(
+            self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF, self._c_ptr(c), x.ptr, N, L.stream()),
+            "zf_flow_sample")
+        return x
+
     def log_prob(self, x: DeviceArray, c=None, out=None, nll_sum: Optional[DeviceArray] = None,
                  op_begin=0, op_end=None, ld_in=None):
         """Flow.__call__ (flow.py:22-48) as one fused launch (+ the NLL reduce)."""

@@ -11,7 +11,7 @@ from .bijectors import Bijector, Chain, _has_stats, _prep_c
 from .distributions import Beta, Distribution
 from .engine import Program
 from .module import Module, current_scope
-from .random import PRNGKey
+from .random import PRNGKey, key_to_seed
 
 __all__ = ["Flow", "BoundFlow"]
 
@@ -60,11 +60,12 @@ class Flow(Module):
             size = c.shape[0]
         if self.latent.dim is None:
             raise ValueError("latent dim unknown: call log_prob (or init) first")
-        z = self.latent.sample(size, PRNGKey(seed))
-        cd, _ = _prep_c(c)
-        prog = self._program(scope.variables, z.shape[1], 0 if cd is None else cd.shape[1])
-        x = prog.inverse(L.DeviceArray.from_numpy(z), cd)
-        return x.numpy()
+        cd, c_dev = _prep_c(c)
+        if cd is not None and cd.shape[0] != size:
+            raise ValueError("conditions must have one row per sample")
+        prog = self._program(scope.variables, self.latent.dim, 0 if cd is None else cd.shape[1])
+        x = prog.sample(size, key_to_seed(PRNGKey(seed)), cd)
+        return x if c_dev else x.numpy()
 
     def _steps(self, x, c=None, *, inverse: bool = False):
         """Per-bijector intermediates (flow.py:80-95), one segment launch each."""

@@ -1,8 +1,9 @@
 """Seeds for init / sample (stand-in for ``jax.random.PRNGKey``).
 
-JAX's threefry stream cannot be reproduced without JAX, so parameter init and
-latent sampling are seeded numpy Generators: same distributions, different
-draws (parity for sampling is statistical)."""
+JAX's threefry stream cannot be reproduced without JAX: parameter init uses
+seeded numpy Generators, latent sampling the device's counter-based Philox
+generator keyed by ``key_to_seed(key)`` — same distributions, different draws
+(parity for sampling is statistical; DESIGN.md §2 sampling)."""
 
 from __future__ import annotations
 
@@ -24,3 +25,18 @@ def as_generator(key) -> np.random.Generator:
         return np.random.default_rng(int(key))
     arr = np.asarray(key, dtype=np.uint64).ravel()
     return np.random.default_rng([int(v) for v in arr])
+
+
+def key_to_seed(key) -> int:
+    """64-bit device seed of a key (``PRNGKey`` array, int, or None)."""
+    if key is None:
+        return 0
+    if isinstance(key, (int, np.integer)):
+        return int(key) & 0xFFFFFFFFFFFFFFFF
+    arr = np.asarray(key).astype(np.uint64).ravel()
+    if arr.size == 2:
+        return (int(arr[0]) << 32) | int(arr[1])
+    h = 0
+    for v in arr:
+        h = (h * 0x9E3779B97F4A7C15 + int(v)) & 0xFFFFFFFFFFFFFFFF
+    return h
