@@ -7,10 +7,11 @@ Public surface mirrors the reference package (src/zenflow/__init__.py):
 in include/zenflow_amd.h."""
 
 from .flow import BoundFlow, Flow
-from . import bijectors, distributions, utils
+from . import bijectors, distributions, io, utils
+from .io import load_variables, save_variables
 from .random import PRNGKey
 
-__all__ = "Flow", "train", "BoundFlow", "PRNGKey"
+__all__ = "Flow", "train", "BoundFlow", "PRNGKey", "save_variables", "load_variables"
 
 
 def train(*args, **kwargs):
