@@ -161,8 +161,8 @@ def load_traffic(kernel_prefix, launches_per_step):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--rows-log2", type=int, default=20, help="rows per GPU = 2^k")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
   const long long row = ((long long)blockIdx.x * kWaves + wave) * kTile + s;
   const bool valid = row < N;
 
-  load_state(xs, xin, row, valid, D, s, hh, F, seed, gen);
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;  // logical dim j is stored in column (j + rot) mod D
   wave_lds_sync();

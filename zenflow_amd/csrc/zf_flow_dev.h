@@ -116,6 +116,17 @@ __device__ __forceinline__ void bias_tile(const float* __restrict__ bt, int hh, 
   for (int r4 = 0; r4 < 4; ++r4) b[r4] = p[r4];
 }
 
+// The same bias tile as an accumulator initialiser: a layer's MFMAs then
+// accumulate onto its bias (no separate add, no zero fill).
+__device__ __forceinline__ floatx16 bias_acc(const float* __restrict__ bt, int hh) {
+  floatx4 b[4];
+  bias_tile(bt, hh, b);
+  floatx16 a;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = b[r >> 2][r & 3];
+  return a;
+}
+
 __device__ __forceinline__ int pmod(int a, int m) {
   int r = a % m;
   return r < 0 ? r + m : r;
@@ -205,7 +216,7 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
   const int DCp = 2 * KS0;
   const float* bn = blob + op.bn;
 #pragma unroll
-  for (int o = 0; o < T; ++o) hb[o] = floatx16{0};
+  for (int o = 0; o < T; ++o) hb[o] = bias_acc(blob + op.b[0] + o * 32, hh);
   for (int ks = 0; ks < KS0; ++ks) {
     const int k = 2 * ks + hh;
     float v = 0.f;
@@ -218,12 +229,9 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
       hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
   }
 #pragma unroll
-  for (int o = 0; o < T; ++o) {
-    floatx4 bv[4];
-    bias_tile(blob + op.b[0] + o * 32, hh, bv);
+  for (int o = 0; o < T; ++o)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r] + bv[r >> 2][r & 3]);
-  }
+    for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
 }
 
 // latent.log_prob(z) + log_det, nan_to_num (flow.py:41-48;

@@ -208,7 +208,8 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
 // prefetch the next group into the next slot, then this group's MFMAs.
 template <int NL, int GT, int NBUF, int NOUT, int Q>
 __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
-                                        floatx16 (&acc)[NOUT], int lane) {
+                                        floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                        int hh) {
   constexpr int kBuf = group_bytes(GT, kX3T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -223,17 +224,35 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   }
   const int nb = (p.buf + 1 == NBUF) ? 0 : p.buf + 1;
   if (p.lead >= 0) x3_issue_next<NL, GT>(x3, p, p.wbuf + nb * kBuf, lane);
-  x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+  if (bias != nullptr) {
+    // Bias of a layer that started from zero: loaded here, in the layer's last
+    // step (its earlier input tiles are dead by now), added after the MFMAs.
+    floatx16 bt[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+    x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] += bt[o];
+  } else {
+    x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+  }
   p.buf = nb;
   p.g += 1;
 }
 
 // A whole streamed Dense layer: kX3T / GT groups.
+// `bias_last`: bias tiles added after the last step (nullptr: acc already
+// holds the bias).
 template <int NL, int GT, int NBUF, int NOUT, int Q = 0>
 __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
-                                         floatx16 (&acc)[NOUT], int lane) {
-  x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane);
-  if constexpr (Q + 1 < kX3T / GT) x3_layer<NL, GT, NBUF, NOUT, Q + 1>(x3, p, hb, acc, lane);
+                                         floatx16 (&acc)[NOUT], int lane, const float* bias_last = nullptr,
+                                         int hh = 0) {
+  if constexpr (Q + 1 < kX3T / GT) {
+    x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane, nullptr, hh);
+    x3_layer<NL, GT, NBUF, NOUT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
+  } else {
+    x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane, bias_last, hh);
+  }
 }
 
 // squareplus with a Newton-corrected reciprocal square root (one
@@ -288,7 +307,7 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
     floatx4* dst = reinterpret_cast<floatx4*>(lsm);
     for (int i = threadIdx.x; i < small4 / 4; i += NW * 64) dst[i] = src[i];
   }
-  load_state(xs, xin, row, valid, D, s, hh, F, seed, gen);
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;
   __syncthreads();
@@ -331,16 +350,13 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
       auto hidden = [&](int l) {
         floatx16 acc[kX3T];
 #pragma unroll
-        for (int o = 0; o < kX3T; ++o) acc[o] = floatx16{0};
+        for (int o = 0; o < kX3T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
         x3_layer<NL, GT, NBUF, kX3T>(x3, pipe, hb, acc, lane);
         X3_MARK(5);
 #pragma unroll
-        for (int o = 0; o < kX3T; ++o) {
-          floatx4 bv[4];
-          bias_tile(sp + op.b[l] + o * 32, hh, bv);
+        for (int o = 0; o < kX3T; ++o)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r] + bv[r >> 2][r & 3]);
-        }
+          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
       };
       for (int l = 1; l < op.n_hidden; ++l) hidden(l);
       // Last Dense (:346-347): lane half h, tile o, register r = parameter
@@ -349,16 +365,13 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
 #pragma unroll
       for (int o = 0; o < TL; ++o) pa[o] = floatx16{0};
       X3_MARK(6);
-      x3_layer<NL, GT, NBUF, TL>(x3, pipe, hb, pa, lane);
+      x3_layer<NL, GT, NBUF, TL>(x3, pipe, hb, pa, lane, sp + op.x3_blast, hh);
       X3_MARK(7);
       float P[TL * 16];
 #pragma unroll
-      for (int o = 0; o < TL; ++o) {
-        floatx4 bv[4];
-        bias_tile(sp + op.x3_blast + o * 32, hh, bv);
+      for (int o = 0; o < TL; ++o)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r] + bv[r >> 2][r & 3];
-      }
+        for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r];
       // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
       const int dt = op.dt;
       float ldv = 0.f;
