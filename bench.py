@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-spline-kernel", action="store_true")
+    ap.add_argument("--force-rccl", action="store_true", help="RCCL all-reduce even at world size 1 (plumbing check)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -216,8 +217,10 @@ def main():
     ws = prog.workspace(N)
     lib = L.load_library()
     comm = None
-    if world > 1:
+    if world > 1 or args.force_rccl:
         def bcast(b):
+            if td is None:  # single process: nothing to exchange
+                return b
             obj = [b]
             td.broadcast_object_list(obj, src=0)
             return obj[0]
