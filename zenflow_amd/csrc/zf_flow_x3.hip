@@ -401,7 +401,7 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
         for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
         float* xp = xs + pmod(hh + rot, D) * 32 + s;
         const float xv = *xp;
-        const RqsBin bin = rqs_bin_regs_sl<!INV, K>(xv, w, hg, sl, [](float v) { return squareplus_rsq(v); });
+        const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl, [](float v) { return v == 0.f ? 1.f : squareplus_rsq(v); });
         float yv;
         if (!INV) {
           float l;

@@ -162,6 +162,45 @@ __device__ __forceinline__ RqsBin rqs_bin_regs_sl(float v, const float (&w)[K], 
   return b;
 }
 
+// rqs_bin_regs_sl for knots known to be strictly increasing (every width and
+// height > 0, as normalize_spline_params guarantees: each is >= c > 0) and
+// raw slope logits mapped by squareplus: the bin is the last knot <= v, so
+// the count / fallback bookkeeping of the general version drops out, and the
+// boundary derivative 1 is carried as the logit 0 (squareplus(0) == 1
+// exactly).  Results equal rqs_bin_regs_sl's for such inputs, including the
+// NaN fill at idx == K (utils.py:224-230).
+template <bool FWD, int K, class TF>
+__device__ __forceinline__ RqsBin rqs_bin_monotone(float v, const float (&w)[K], const float (&h)[K],
+                                                   const float (&sl)[K - 1], const TF& sp) {
+  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  float lo = 0.f, hi = (K > 1) ? sl[0] : 0.f;  // logits of dk, dk+1 at the current bin
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) {
+      sxk = xk; syk = yk; sw = w[j]; sh = h[j];
+      lo = (j >= 1) ? sl[j - 1] : 0.f;
+      hi = (j + 1 < K) ? sl[j] : 0.f;
+    }
+    xk = xk + w[j];
+    yk = yk + h[j];
+  }
+  {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { sxk = xk; syk = yk; sw = qnan(); sh = qnan(); lo = 0.f; hi = qnan(); }
+  }
+  RqsBin b;
+  b.xk = sxk;
+  b.yk = syk;
+  b.w = sw;
+  b.h = sh;
+  b.dk = sp(lo);
+  b.dkp1 = sp(hi);
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+
 // utils.py:121-139 — forward value and per-dim log|dy/dx|.
 __device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
   const float zr = (x - b.xk) / b.w;               // :122
