@@ -367,7 +367,6 @@ struct zf_flow {
   float* d_blob = nullptr;
   void* d_x3 = nullptr;       // bf16x3 weight-group stream (x3 kernel), or null
   int x3_K = 0;
-  int x3_variant = 0;         // launch shape of the x3 kernel (zf_flow_x3.hip)
   int device = 0;
 };
 
@@ -508,7 +507,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       for (int l = 0; l < op.n_hidden; ++l) d.b[l] = take((int64_t)T * 32);
       d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
       d.x3 = -1;
-      if (x3) d.x3_blast = take((int64_t)zf::x3_last_tiles(x3K) * 32);
+      if (x3) d.x3_blast = take((int64_t)zf::x3_pairs(desc) * zf::x3_last_tiles(x3K) * 32);
     } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
       d.sb = take(8 * desc.dim);
     }
@@ -583,16 +582,10 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
     }
   }
   std::vector<uint16_t> x3s;
-  if (x3) {
-    const char* v = std::getenv("ZF_X3_VARIANT");
-    // default: 4-wave blocks, one-tile groups, three blocks per CU (zf_flow_x3.hip)
-    h->x3_variant = (v && v[0] >= '0' && v[0] <= '4') ? v[0] - '0' : 4;
-    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) > 160 * 1024) h->x3_variant = 4;
-    if (zf::x3_lds_bytes(h->x3_variant, F.small_floats, desc.dim) <= 160 * 1024) {
-      zf::x3_pack(desc, nat, zf::x3_group_tiles(h->x3_variant), F, P, x3s);
-      F.x3_ok = 1;
-      h->x3_K = x3K;
-    }
+  if (x3 && zf::x3_lds_bytes(T, desc.dim) <= 160 * 1024) {
+    zf::x3_pack(desc, nat, T, F, P, x3s);
+    F.x3_ok = 1;
+    h->x3_K = x3K;
   }
   const bool use_x3 = F.x3_ok != 0;
   int rcd = ZF_OK;
@@ -653,8 +646,7 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.desc = h->d_desc; a.blob = h->d_blob; a.x3 = h->d_x3;
     a.x = x; a.c = c; a.y = y; a.ld_in = ld_in; a.ld_out = ld_out; a.lp = lp; a.part = part;
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
-    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.variant = h->x3_variant;
-    a.small_floats = h->host.small_floats;
+    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.T = h->host.HP / 32;
     a.seed = seed;
     a.gen = gen;
     a.stream = (hipStream_t)stream;

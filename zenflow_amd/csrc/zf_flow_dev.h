@@ -316,15 +316,15 @@ struct X3Launch {
   long long N;
   unsigned long long seed;
   int gen;  // 1: draw the input rows from the latent (zf_flow_sample)
-  int K, D, variant, small_floats;
+  int K, D, T;  // knots, dim, hidden tiles (4: width <= 128, 8: <= 256)
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
-int x3_group_tiles(int variant);
-size_t x3_lds_bytes(int variant, int small_floats, int D);
-void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, float* packed,
+int x3_pairs(const zf_flow_desc& desc);
+size_t x3_lds_bytes(int T, int D);
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);
 
 }  // namespace zf

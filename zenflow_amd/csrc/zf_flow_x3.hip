@@ -42,9 +42,9 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kX3T = 4;  // hidden tiles (hidden padded to 128)
-// Bytes of one weight group covering GT input tiles: [tl][s][o][part] x 1 KiB.
-constexpr int group_bytes(int GT, int NOUT) { return GT * 2 * NOUT * 3 * 1024; }
+constexpr int kX3Waves = 4;  // waves per block: 128 samples
+// Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
+constexpr int group_bytes(int NOUT) { return 2 * NOUT * 3 * 1024; }
 
 #ifndef ZF_X3_TRACE
 #define ZF_X3_TRACE 0
@@ -99,28 +99,25 @@ __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, co
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
-// One weight group from LDS: input tiles GT*Q .. GT*Q+GT-1 (2 k-steps of 16
-// each) into NOUT output tiles.  Block (tl, s, o, part) is 1 KiB at
-// (((tl*2 + s)*NOUT + o)*3 + part) KiB; lane l's 16 bytes at l*16.
-template <int NOUT, int GT, int Q>
-__device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[kX3T], floatx16 (&acc)[NOUT],
+// One weight group from LDS: input tile Q (2 k-steps of 16) into NOUT
+// output tiles.  Block (s, o, part) is 1 KiB at ((s*NOUT + o)*3 + part) KiB;
+// lane l's 16 bytes at l*16.
+template <int T, int NOUT, int Q>
+__device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
                                          int lane) {
   const char* lb = buf + lane * 16;
 #pragma unroll
-  for (int tl = 0; tl < GT; ++tl) {
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 bh, bm, bl;
+    if (s == 0) split8<0>(hb[Q], bh, bm, bl);
+    else split8<1>(hb[Q], bh, bm, bl);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 bh, bm, bl;
-      if (s == 0) split8<0>(hb[GT * Q + tl], bh, bm, bl);
-      else split8<1>(hb[GT * Q + tl], bh, bm, bl);
-#pragma unroll
-      for (int o = 0; o < NOUT; ++o) {
-        const char* a = lb + ((((tl * 2 + s) * NOUT + o) * 3) << 10);
-        const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
-        const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
-        const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
-        acc[o] = mfma3(ah, am, al, bh, bm, bl, acc[o]);
-      }
+    for (int o = 0; o < NOUT; ++o) {
+      const char* a = lb + (((s * NOUT + o) * 3) << 10);
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
+      const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
+      acc[o] = mfma3(ah, am, al, bh, bm, bl, acc[o]);
     }
   }
 }
@@ -128,7 +125,9 @@ __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[k
 // The group stream of the NSC being computed (byte offsets into the x3
 // blob), set up at NSC entry from the op's scalar fields: the per-step
 // prefetch then needs no memory access of its own (a scalar load there would
-// make its lgkmcnt wait drain the step's LDS reads too).
+// make its lgkmcnt wait drain the step's LDS reads too).  Groups in order:
+// hidden layers (T groups each), then the last layer (T groups per pair of
+// transformed dims).
 struct X3Span {
   long long base;       // group 0 of this NSC
   long long next_base;  // group 0 of the next NSC in execution order within range, or -1
@@ -137,23 +136,23 @@ struct X3Span {
   int next_pieces;      // KiB pieces of the next NSC's group 0
 };
 
-template <int GT>
+template <int T>
 __device__ __forceinline__ int first_pieces(const DevOp& op) {
-  return (op.n_hidden > 1 ? group_bytes(GT, kX3T) : group_bytes(GT, op.x3_tlast)) >> 10;
+  return (op.n_hidden > 1 ? group_bytes(T) : group_bytes(op.x3_tlast)) >> 10;
 }
 
-template <int GT, bool INV>
+template <int T, bool INV>
 __device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int oi, int op_begin, int op_end) {
   const DevOp& op = F->ops[oi];
   X3Span sp;
   sp.base = op.x3;
   sp.G = op.x3_groups;
-  sp.nhid = (kX3T / GT) * (op.n_hidden - 1);
-  sp.last_pieces = group_bytes(GT, op.x3_tlast) >> 10;
+  sp.nhid = T * (op.n_hidden - 1);
+  sp.last_pieces = group_bytes(op.x3_tlast) >> 10;
   const int n = op.x3_next[INV ? 1 : 0];
   if (n >= op_begin && n < op_end) {
     sp.next_base = F->ops[n].x3;
-    sp.next_pieces = first_pieces<GT>(F->ops[n]);
+    sp.next_pieces = first_pieces<T>(F->ops[n]);
   } else {
     sp.next_base = -1;
     sp.next_pieces = 0;
@@ -164,28 +163,26 @@ __device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int o
 // Issue the DMA of one group into an LDS buffer: 1 KiB pieces (one
 // global_load_lds_dwordx4 per wave: wave-uniform LDS base, lane*16 implied)
 // spread over the block's waves.
-template <int NW>
-__device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave,
-                                       int lane) {
-  for (int p = wave; p < pieces; p += NW)
+__device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave, int lane) {
+  for (int p = wave; p < pieces; p += kX3Waves)
     __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
                                      (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
 }
 
 // Block-wide weight-group pipeline state (every field wave-uniform).
 struct X3Pipe {
-  char* wbuf;   // [NBUF][group bytes] LDS ring
-  int buf;      // ring slot holding the group this wave computes next
+  char* wbuf;   // [2][group bytes] LDS double buffer
+  int buf;      // buffer holding the group this wave computes next
   int g;        // index of that group within the current NSC
   X3Span span;  // current NSC's group stream
-  int lead;     // index of this wave among the NL DMA-issuing waves, or -1
+  int wave;
 };
 
 // DMA the group after group p.g (the next one of this NSC, or group 0 of
 // the next NSC) into `dst`; nothing at the end of the stream.
-template <int NL, int GT>
+template <int T>
 __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
-  constexpr int kHid = group_bytes(GT, kX3T);
+  constexpr int kHid = group_bytes(T);
   const int g = p.g + 1;
   long long off;
   int pieces;
@@ -200,58 +197,48 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
     off = p.span.next_base;
     pieces = p.span.next_pieces;
   }
-  x3_dma<NL>(x3 + off, dst, pieces, p.lead, lane);
+  x3_dma(x3 + off, dst, pieces, p.wave, lane);
 }
 
 // One pipeline step: wait for this wave's DMAs, block barrier (the group in
-// slot `buf` is complete and the slot after it is free), the issuing waves
-// prefetch the next group into the next slot, then this group's MFMAs.
-template <int NL, int GT, int NBUF, int NOUT, int Q>
-__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
+// buffer `buf` is complete and the other buffer is free), prefetch the next
+// group into it, then this group's MFMAs.  `bias` (optional): bias tiles of
+// a layer that started from zero, loaded here — in the layer's last step,
+// when its earlier input tiles are dead — and added after the MFMAs.
+template <int T, int NOUT, int Q>
+__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
                                         int hh) {
-  constexpr int kBuf = group_bytes(GT, kX3T);
+  constexpr int kBuf = group_bytes(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   X3_MARK(2);
-  if constexpr (NBUF == 3) {
-    // Offset half-blocks: the wave whose step ends in a VALU tail (the
-    // layer's last group -> epilogue / spline) issues its MFMAs first, so
-    // that tail overlaps the partner wave's MFMAs on the same SIMD.
-    if constexpr (Q + 1 == kX3T / GT) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-  }
-  const int nb = (p.buf + 1 == NBUF) ? 0 : p.buf + 1;
-  if (p.lead >= 0) x3_issue_next<NL, GT>(x3, p, p.wbuf + nb * kBuf, lane);
+  x3_issue_next<T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   if (bias != nullptr) {
-    // Bias of a layer that started from zero: loaded here, in the layer's last
-    // step (its earlier input tiles are dead by now), added after the MFMAs.
     floatx16 bt[NOUT];
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-    x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+    x3_group<T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) acc[o] += bt[o];
   } else {
-    x3_group<NOUT, GT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+    x3_group<T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
   }
-  p.buf = nb;
+  p.buf ^= 1;
   p.g += 1;
 }
 
-// A whole streamed Dense layer: kX3T / GT groups.
-// `bias_last`: bias tiles added after the last step (nullptr: acc already
-// holds the bias).
-template <int NL, int GT, int NBUF, int NOUT, int Q = 0>
-__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[kX3T],
+// A whole streamed Dense layer: T groups (one per input tile).
+template <int T, int NOUT, int Q = 0>
+__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[T],
                                          floatx16 (&acc)[NOUT], int lane, const float* bias_last = nullptr,
                                          int hh = 0) {
-  if constexpr (Q + 1 < kX3T / GT) {
-    x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane, nullptr, hh);
-    x3_layer<NL, GT, NBUF, NOUT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
+  if constexpr (Q + 1 < T) {
+    x3_step<T, NOUT, Q>(x3, p, hb, acc, lane, nullptr, hh);
+    x3_layer<T, NOUT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
   } else {
-    x3_step<NL, GT, NBUF, NOUT, Q>(x3, p, hb, acc, lane, bias_last, hh);
+    x3_step<T, NOUT, Q>(x3, p, hb, acc, lane, bias_last, hh);
   }
 }
 
@@ -265,22 +252,21 @@ __device__ __forceinline__ float squareplus_rsq(float x) {
   return 0.5f * (x + sq);
 }
 
-// PIPE 0: every wave issues DMA pieces and all waves step in lockstep
-// (NBUF = 2).  PIPE 1: the block runs as two half-blocks offset by one
-// group — waves [0, NW/2) issue every DMA and compute group t while waves
-// [NW/2, NW) compute group t-1 (NBUF = 3) — so one half's VALU phases
-// (spline, swish epilogues, layer 0) overlap the other half's MFMAs on the
-// same SIMD.  PIPE 2: lockstep, small parameters read from global memory
-// (L2-resident) instead of LDS, so that three 4-wave blocks fit a CU's LDS
-// (3 waves per SIMD, <= 168 VGPRs).
-template <int K, int NW, int GT, int PIPE, bool INV>
-__global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x3(
+// Block: 4 waves x 32 samples, one 32-row input tile per weight group,
+// double-buffered in LDS.  Small parameters (BatchNorm, first Dense, biases,
+// ShiftBounds rows) are read from global memory (L2-resident), so the LDS
+// footprint is 2 groups + the state: 50 KiB at T = 4 (3 blocks = 3 waves per
+// SIMD, <= 168 VGPRs), 104 KiB at T = 8 (hidden 256: one block per CU, the
+// 8 + 8 accumulator tiles need one wave's whole register file).
+template <int K, int T, bool PAIRS, bool INV>
+__global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
     double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N,
     unsigned long long seed, int gen) {
-  constexpr int TL = (3 * K - 1 + 15) / 16;  // last-layer tiles: 16 parameters per lane half
+  constexpr int TL = (3 * K - 1 + 15) / 16;  // last-layer tiles per dim pair: 16 parameters per lane half
+  constexpr int NW = kX3Waves;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int D = F->D;
   const int C = F->C;
@@ -288,35 +274,25 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
   const int lane = threadIdx.x & 63;
   const int s = lane & 31;
   const int hh = lane >> 5;
-  constexpr int kBuf = group_bytes(GT, kX3T);
-  constexpr int NBUF = PIPE == 1 ? 3 : 2;
-  constexpr int NL = PIPE == 1 ? NW / 2 : NW;  // DMA-issuing waves
-  constexpr bool kSmallLds = PIPE != 2;
-  // LDS: [NBUF][kBuf] weight ring | small parameters | [NW][D][32] state | [NW] partials
-  const int small4 = kSmallLds ? (F->small_floats + 3) & ~3 : 0;
-  float* lsm = reinterpret_cast<float*>(lds + NBUF * kBuf);
-  const float* sp = kSmallLds ? lsm : blob;
-  float* xs = lsm + small4 + wave * (32 * D);
-  double* s_part = reinterpret_cast<double*>(lsm + small4 + NW * 32 * D);
+  constexpr int kBuf = group_bytes(T);
+  // LDS: [2][kBuf] weight groups | [NW][D][32] state | [NW] partials
+  float* xs = reinterpret_cast<float*>(lds + 2 * kBuf) + wave * (32 * D);
+  double* s_part = reinterpret_cast<double*>(reinterpret_cast<float*>(lds + 2 * kBuf) + NW * 32 * D);
+  const float* sp = blob;
   const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
   const bool valid = row < N;
 
   X3_MARK(0);
-  {  // small parameters -> LDS (before any DMA is in flight)
-    const floatx4* src = reinterpret_cast<const floatx4*>(blob);
-    floatx4* dst = reinterpret_cast<floatx4*>(lsm);
-    for (int i = threadIdx.x; i < small4 / 4; i += NW * 64) dst[i] = src[i];
-  }
   load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;
-  __syncthreads();
+  wave_lds_sync();
 
   X3Pipe pipe;
   pipe.wbuf = lds;
   pipe.buf = 0;
   pipe.g = 0;
-  pipe.lead = wave < NL ? wave : -1;
+  pipe.wave = wave;
   {  // group 0 of the first NSC in execution order goes out now
     int first = -1;
     const int nq = op_end - op_begin;
@@ -324,10 +300,8 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
       const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
       if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
     }
-    if (first >= 0 && pipe.lead >= 0)
-      x3_dma<NL>(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<GT>(F->ops[first]), pipe.lead, lane);
+    if (first >= 0) x3_dma(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<T>(F->ops[first]), wave, lane);
   }
-  if (PIPE == 1 && pipe.lead < 0) __syncthreads();  // trailing half starts one step late
 
   const KnotConsts kc(K);
   const int nq = op_end - op_begin;
@@ -340,93 +314,104 @@ __global__ __launch_bounds__(NW * 64, PIPE == 2 ? 3 : 8 / NW) void flow_kernel_x
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
       shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
-      pipe.span = make_span<GT, INV>(F, oi, op_begin, op_end);
+      pipe.span = make_span<T, INV>(F, oi, op_begin, op_end);
       pipe.g = 0;
-      floatx16 hb[kX3T];
+      floatx16 hb[T];
       X3_MARK(3);
-      layer0<kX3T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
+      layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
       X3_MARK(4);
-      // Hidden layers 1..n_hidden-1 (:343-345), kX3T / GT groups each.
-      auto hidden = [&](int l) {
-        floatx16 acc[kX3T];
+      // Hidden layers 1..n_hidden-1 (:343-345), T groups each; the biases
+      // seed the accumulators.
+      for (int l = 1; l < op.n_hidden; ++l) {
+        floatx16 acc[T];
 #pragma unroll
-        for (int o = 0; o < kX3T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
-        x3_layer<NL, GT, NBUF, kX3T>(x3, pipe, hb, acc, lane);
+        for (int o = 0; o < T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
+        x3_layer<T, T>(x3, pipe, hb, acc, lane);
         X3_MARK(5);
 #pragma unroll
-        for (int o = 0; o < kX3T; ++o)
+        for (int o = 0; o < T; ++o)
 #pragma unroll
           for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
-      };
-      for (int l = 1; l < op.n_hidden; ++l) hidden(l);
-      // Last Dense (:346-347): lane half h, tile o, register r = parameter
-      // 16*o + r of transformed dim h.
-      floatx16 pa[TL];
-#pragma unroll
-      for (int o = 0; o < TL; ++o) pa[o] = floatx16{0};
-      X3_MARK(6);
-      x3_layer<NL, GT, NBUF, TL>(x3, pipe, hb, pa, lane, sp + op.x3_blast, hh);
-      X3_MARK(7);
-      float P[TL * 16];
-#pragma unroll
-      for (int o = 0; o < TL; ++o)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r];
-      // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
+      }
+      // Last Dense (:346-347), one pair of transformed dims at a time: lane
+      // half h, tile o, register r = parameter 16*o + r of dim 2*pair + h.
       const int dt = op.dt;
-      float ldv = 0.f;
-      const bool act = hh < dt;  // lane half h transforms dim h (idle half when dt == 1)
-      {
-        float w[K], hg[K];
-        float sx = 0.f, sy = 0.f;
+      float ldn = 0.f;  // this coupling's log-det, summed in dim order (utils.py:139)
+      // PAIRS == false: one pair (dt <= 2), and the hidden activations are
+      // dead once the last layer has consumed them.
+      const int npair = PAIRS ? (dt + 1) / 2 : 1;
+      for (int pr = 0; pr < npair; ++pr) {
+        // The bias seeds the accumulators when the hidden activations stay
+        // live across pairs anyway; otherwise it joins in the last step, when
+        // the first input tiles are dead (fewer registers at the peak).
+        const float* bl = sp + op.x3_blast + pr * TL * 32;
+        floatx16 pa[TL];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-          w[j] = squareplus_rsq(P[j]);
-          hg[j] = squareplus_rsq(P[K + j]);
-          sx = sx + w[j];
-          sy = sy + hg[j];
+        for (int o = 0; o < TL; ++o) pa[o] = PAIRS ? bias_acc(bl + o * 32, hh) : floatx16{0};
+        X3_MARK(6);
+        x3_layer<T, TL>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
+        X3_MARK(7);
+        float P[TL * 16];
+#pragma unroll
+        for (int o = 0; o < TL; ++o)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r];
+        // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
+        const int d = 2 * pr + hh;
+        const bool act = d < dt;  // the upper half idles on an odd last dim
+        float ldv = 0.f;
+        {
+          float w[K], hg[K];
+          float sx = 0.f, sy = 0.f;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
+            w[j] = squareplus_rsq(P[j]);
+            hg[j] = squareplus_rsq(P[K + j]);
+            sx = sx + w[j];
+            sy = sy + hg[j];
+          }
+          // (v / sum + c) / (1 + c K) as one fma per knot: the parameters
+          // themselves already differ from the reference's in the last ulp
+          // (GEMM summation order), so correctly rounded divisions buy nothing.
+          const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
+          const float bc = kc.c * kc.rnorm;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            w[j] = __builtin_fmaf(w[j], ax, bc);
+            hg[j] = __builtin_fmaf(hg[j], ay, bc);
+          }
+          float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
+#pragma unroll
+          for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
+          float* xp = xs + pmod((act ? d : 0) + rot, D) * 32 + s;
+          const float xv = *xp;
+          const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
+                                                       [](float v) { return v == 0.f ? 1.f : squareplus_rsq(v); });
+          float yv;
+          if (!INV) {
+            float l;
+            rqs_forward_eval(xv, bin, yv, l);
+            ldv = act ? l : 0.f;
+          } else {
+            yv = rqs_inverse_eval(xv, bin);
+          }
+          if (act) *xp = yv;
         }
-        // (v / sum + c) / (1 + c K) as one fma per knot: the parameters
-        // themselves already differ from the reference's in the last ulp
-        // (GEMM summation order), so correctly rounded divisions buy nothing.
-        const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
-        const float bc = kc.c * kc.rnorm;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          w[j] = __builtin_fmaf(w[j], ax, bc);
-          hg[j] = __builtin_fmaf(hg[j], ay, bc);
-        }
-        float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
-#pragma unroll
-        for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
-        float* xp = xs + pmod(hh + rot, D) * 32 + s;
-        const float xv = *xp;
-        const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl, [](float v) { return v == 0.f ? 1.f : squareplus_rsq(v); });
-        float yv;
+        wave_lds_sync();
+        X3_MARK(8);
         if (!INV) {
-          float l;
-          rqs_forward_eval(xv, bin, yv, l);
-          ldv = act ? l : 0.f;
-        } else {
-          yv = rqs_inverse_eval(xv, bin);
+          const float other = __shfl_xor(ldv, 32);
+          ldn = ldn + (hh == 0 ? ldv : other);
+          if (2 * pr + 1 < dt) ldn = ldn + (hh == 0 ? other : ldv);
         }
-        if (act) *xp = yv;
       }
-      wave_lds_sync();
-      X3_MARK(8);
-      if (!INV) {  // log_det.sum(axis=1) in dim order (utils.py:139), Chain += (bijectors.py:110)
-        const float other = __shfl_xor(ldv, 32);
-        float ldc = hh == 0 ? ldv : other;
-        if (dt == 2) ldc = ldc + (hh == 0 ? other : ldv);
-        ld = ld + ldc;
-      }
+      if (!INV) ld = ld + ldn;  // Chain: log_det += ld (bijectors.py:110)
     }
   }
 
-  if (PIPE == 1 && pipe.lead >= 0) __syncthreads();  // leading half: matching trailing step
   X3_MARK(9);
-  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial,
-                    NW * kTile / 128, nparts, y_out, ld_out, s_part);
+  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, nparts, y_out,
+                    ld_out, s_part);
   X3_MARK(10);
 }
 
@@ -447,11 +432,11 @@ float bf16_f(uint16_t b) {
 
 }  // namespace
 
-// hidden widths padded to 128, one knot count in {8, 16}, <= 2 transformed dims.
+// One knot count for all couplings and one of the instantiated shapes
+// (launch_flow_x3).
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   const char* env = std::getenv("ZF_DISABLE_X3");
   if (env && env[0] == '1') return false;
-  if (HP != 128) return false;
   int K = 0;
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
@@ -459,18 +444,22 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }
-  if (K != 8 && K != 16) return false;
-  if (desc.dim / 2 > 2) return false;
+  const int dt = desc.dim / 2;
+  const bool narrow = HP == 128 && (K == 8 || K == 16) && dt <= 2;
+  const bool wide = HP == 256 && (K == 16 || K == 32) && dt <= 8;
+  if (!narrow && !wide) return false;
   *K_out = K;
   return true;
 }
 
 int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
 
+int x3_pairs(const zf_flow_desc& desc) { return (desc.dim / 2 + 1) / 2; }
+
 // Pack the group streams (bf16 hi/mid/lo A fragments) of every NSC and the
 // row-permuted last-layer biases (into `packed` at F.ops[i].x3_blast, which
-// the caller allocated with x3_last_tiles(K)*32 floats).
-void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, float* packed,
+// the caller allocated with x3_pairs * x3_last_tiles(K) * 32 floats).
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream) {
   stream.clear();
   int prev = -1;
@@ -485,24 +474,24 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, flo
     if (op.kind != ZF_OP_NSC) continue;
     DevOp& d = F.ops[i];
     const int dt = desc.dim / 2, K = op.knots, S = 3 * K - 1;
-    const int TL = x3_last_tiles(K);
+    const int TL = x3_last_tiles(K), NP = x3_pairs(desc);
     d.x3 = (long long)stream.size() * 2;
     d.x3_tlast = TL;
-    d.x3_groups = (kX3T / GT) * op.n_hidden;
+    d.x3_groups = T * (op.n_hidden - 1) + T * NP;
     for (int l = 1; l <= op.n_hidden; ++l) {
       const bool last = (l == op.n_hidden);
       const int in = op.hidden[l - 1];
       const int out = last ? dt * S : op.hidden[l];
-      const int NOUT = last ? TL : kX3T;
+      const int NOUT = last ? TL : T;
       const float* W = nat + op.off_w[l];
-      for (int q = 0; q < kX3T / GT; ++q)
-        for (int tl = 0; tl < GT; ++tl)
+      for (int pr = 0; pr < (last ? NP : 1); ++pr)
+        for (int q = 0; q < T; ++q)
           for (int s = 0; s < 2; ++s)
             for (int o = 0; o < NOUT; ++o) {
               uint16_t part[3][64][8];
               for (int ln = 0; ln < 64; ++ln)
                 for (int j = 0; j < 8; ++j) {
-                  const int kstep = 2 * (GT * q + tl) + s;
+                  const int kstep = 2 * q + s;
                   const int k = 16 * kstep + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3);
                   const int rho = ln & 31;
                   int col;
@@ -511,7 +500,8 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, flo
                     if (col >= out) col = -1;
                   } else {
                     const int h = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3), jp = 16 * o + r;
-                    col = (h < dt && jp < S) ? h * S + jp : -1;
+                    const int dd = 2 * pr + h;
+                    col = (dd < dt && jp < S) ? dd * S + jp : -1;
                   }
                   const float x = (k < in && col >= 0) ? W[(int64_t)k * out + col] : 0.f;
                   const uint16_t bh = bf16_rne(x);
@@ -526,57 +516,49 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int GT, DevFlow& F, flo
               stream.insert(stream.end(), pp, pp + 3 * 64 * 8);
             }
     }
-    // permuted last bias: [o][lane half h][r] = bias[h*S + 16o + r]
+    // permuted last bias: [pair][o][lane half h][r] = bias[(2 pair + h) S + 16o + r]
     const float* B = nat + op.off_b[op.n_hidden];
-    for (int o = 0; o < TL; ++o)
-      for (int h = 0; h < 2; ++h)
-        for (int r = 0; r < 16; ++r) {
-          const int jp = 16 * o + r;
-          packed[d.x3_blast + (o * 2 + h) * 16 + r] = (h < dt && jp < S) ? B[h * S + jp] : 0.f;
-        }
+    for (int pr = 0; pr < NP; ++pr)
+      for (int o = 0; o < TL; ++o)
+        for (int h = 0; h < 2; ++h)
+          for (int r = 0; r < 16; ++r) {
+            const int jp = 16 * o + r, dd = 2 * pr + h;
+            packed[d.x3_blast + ((pr * TL + o) * 2 + h) * 16 + r] = (dd < dt && jp < S) ? B[dd * S + jp] : 0.f;
+          }
   }
 }
 
-template <int NW, int GT, int PIPE>
-size_t lds_bytes(int small_floats, int D) {
-  return (size_t)(PIPE == 1 ? 3 : 2) * group_bytes(GT, kX3T) + (size_t)(PIPE == 2 ? 0 : (small_floats + 3) & ~3) * 4 +
-         (size_t)NW * 32 * D * 4 + NW * sizeof(double);
+size_t x3_lds_bytes(int T, int D) {
+  return (size_t)2 * group_bytes(T) + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
 }
 
-template <int K, int NW, int GT, int PIPE>
+template <int K, int T, bool PAIRS>
 int launch_x3(const X3Launch& a, bool inverse) {
-  const long long rows = NW * kTile;
+  const long long rows = kX3Waves * kTile;
   const long long grid = (a.N + rows - 1) / rows;
   if (grid > 0x7fffffffLL) return einval("N too large");
-  const size_t lds = lds_bytes<NW, GT, PIPE>(a.small_floats, a.D);
+  const size_t lds = x3_lds_bytes(T, a.D);
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
-    hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, true>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<K, T, PAIRS, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
-    hipLaunchKernelGGL((flow_kernel_x3<K, NW, GT, PIPE, false>), dim3((unsigned)grid), dim3(NW * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<K, T, PAIRS, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
   return ZF_OK;
 }
 
-template <int K>
-int launch_x3_k(const X3Launch& a, bool inverse) {
-  switch (a.variant) {
-    case 1: return launch_x3<K, 4, 1, 0>(a, inverse);  // 4 waves, 1-tile groups, 2 blocks per CU
-    case 2: return launch_x3<K, 8, 2, 1>(a, inverse);  // 8 waves, half-blocks offset by one group
-    case 3: return launch_x3<K, 8, 1, 1>(a, inverse);  // same with 1-tile groups
-    case 4: return launch_x3<K, 4, 1, 2>(a, inverse);  // 4 waves, 3 blocks per CU
-    default: return launch_x3<K, 8, 2, 0>(a, inverse); // 8 waves in lockstep
-  }
-}
-
+// Instantiated shapes (x3_eligible): hidden <= 128 with K 8/16 and dt <= 2
+// (cfg1-4, deep-set); hidden <= 256 with K 16/32, any dt <= 8 (cfg5).
 int launch_flow_x3(const X3Launch& a, bool inverse) {
-  if (a.K == 16) return launch_x3_k<16>(a, inverse);
-  if (a.K == 8) return launch_x3_k<8>(a, inverse);
-  return enotsup("bf16x3 kernel: knots must be 8 or 16");
+  if (a.T == 4 && a.K == 8) return launch_x3<8, 4, false>(a, inverse);
+  if (a.T == 4 && a.K == 16) return launch_x3<16, 4, false>(a, inverse);
+  if (a.T == 8 && a.K == 16) return launch_x3<16, 8, true>(a, inverse);
+  if (a.T == 8 && a.K == 32) return launch_x3<32, 8, true>(a, inverse);
+  return enotsup("bf16x3 kernel: shape not instantiated");
 }
 
 #if ZF_X3_TRACE
@@ -588,17 +570,5 @@ extern "C" int zf_debug_x3_trace(unsigned long long* out, int* counts) {
   return 0;
 }
 #endif
-
-size_t x3_lds_bytes(int variant, int small_floats, int D) {
-  switch (variant) {
-    case 1: return lds_bytes<4, 1, 0>(small_floats, D);
-    case 2: return lds_bytes<8, 2, 1>(small_floats, D);
-    case 3: return lds_bytes<8, 1, 1>(small_floats, D);
-    case 4: return lds_bytes<4, 1, 2>(small_floats, D);
-    default: return lds_bytes<8, 2, 0>(small_floats, D);
-  }
-}
-
-int x3_group_tiles(int variant) { return (variant == 1 || variant == 3 || variant == 4) ? 1 : 2; }
 
 }  // namespace zf
