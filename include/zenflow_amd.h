@@ -243,6 +243,48 @@ int zf_colstats(const float* x, int64_t N, int ncols, int64_t ld, int col_offset
                 double* csum, double* csumsq, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Training — zenflow.train (src/zenflow/train.py:18-138).                    */
+/* ------------------------------------------------------------------------ */
+
+/* optax.adamw / optax.nadamw hyper-parameters (train.py:13-16 default:
+ * nadamw(learning_rate=1e-3); optax defaults b1 0.9, b2 0.999, eps 1e-8,
+ * weight_decay 1e-4). */
+typedef struct zf_optim_desc {
+  float learning_rate, b1, b2, eps, weight_decay;
+  int nesterov; /* 1: nadamw, 0: adamw */
+} zf_optim_desc;
+
+typedef struct zf_trainer zf_trainer_t;
+
+/* A trainer owns a device copy of the natural blob (zf_flow_plan layout:
+ * parameters AND batch statistics), its gradient and the optimiser moments.
+ * param_mask[i] = 1 marks the blob entries that are parameters (updated by
+ * the optimiser), 0 the batch statistics.  ShiftBounds rows carry the margin
+ * in slot 5.  ShiftBounds is supported as the first op only; conditioner
+ * inputs <= 64; batches up to batch_max rows. */
+int zf_trainer_create(const zf_flow_desc* desc, const float* blob_host, int64_t blob_floats,
+                      const unsigned char* param_mask, int64_t batch_max, const zf_optim_desc* opt,
+                      zf_trainer_t** trainer);
+int zf_trainer_destroy(zf_trainer_t* trainer);
+
+/* loss_fn of train.py:64-72 and its gradient (jax.grad): train-mode forward
+ * (batch statistics) of x (B,D), c (B,C) or NULL on the device; loss[0] (fp64,
+ * device) = -mean(log_prob); grad (device, blob layout; NULL: internal) =
+ * d loss / d blob (zero on statistics).  update_stats != 0 also applies the
+ * running-statistics updates (ShiftBounds min/max, BatchNorm momentum). */
+int zf_trainer_loss_grad(zf_trainer_t* trainer, const float* x, const float* c, int64_t B, int update_stats,
+                         double* loss, float* grad, void* stream);
+
+/* step of train.py:80-86: loss_grad with statistics update, then the
+ * optimiser update of the parameters. */
+int zf_trainer_step(zf_trainer_t* trainer, const float* x, const float* c, int64_t B, double* loss,
+                    void* stream);
+
+/* Copy the trainer's natural blob (parameters + statistics) out / in. */
+int zf_trainer_get_blob(zf_trainer_t* trainer, float* blob_host);
+int zf_trainer_set_blob(zf_trainer_t* trainer, const float* blob_host);
+
+/* ------------------------------------------------------------------------ */
 /* RCCL (over xGMI) — all-reduce of the fp64 NLL partial across ranks.       */
 /* ------------------------------------------------------------------------ */
 int zf_rccl_available(void);

@@ -104,9 +104,12 @@ def test_apply_outside_scope_raises():
         nsc(np.zeros((2, 2)))
 
 
-def test_train_is_out_of_scope():
-    with pytest.raises(NotImplementedError):
-        zf.train(None, None, None)
+def test_optimizer_defaults():
+    """train.py:13-16: nadamw(learning_rate=1e-3) with optax's defaults."""
+    o = zf.nadamw()
+    assert (o.learning_rate, o.b1, o.b2, o.eps, o.weight_decay, o.nesterov) == (1e-3, 0.9, 0.999, 1e-8, 1e-4, True)
+    assert zf.adamw(learning_rate=3e-4).nesterov is False
+    assert o.desc().nesterov == 1
 
 
 @pytest.mark.parametrize("n,world", [(10, 3), (1 << 20, 8), (5, 8), (0, 2)])

@@ -52,6 +52,11 @@ class ZfOpDesc(C.Structure):
     ]
 
 
+class ZfOptimDesc(C.Structure):
+    _fields_ = [("learning_rate", C.c_float), ("b1", C.c_float), ("b2", C.c_float), ("eps", C.c_float),
+                ("weight_decay", C.c_float), ("nesterov", C.c_int)]
+
+
 class ZfFlowDesc(C.Structure):
     _fields_ = [
         ("dim", C.c_int32),
@@ -109,6 +114,12 @@ SIGNATURES = {
     "zf_flow_forward": (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "zf_flow_inverse": (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _vp]),
     "zf_flow_sample": (_int, [_vp, _u64, _vp, _vp, _i64, _vp]),
+    "zf_trainer_create": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "zf_trainer_destroy": (_int, [_vp]),
+    "zf_trainer_loss_grad": (_int, [_vp, _vp, _vp, _i64, _int, _vp, _vp, _vp]),
+    "zf_trainer_step": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "zf_trainer_get_blob": (_int, [_vp, _vp]),
+    "zf_trainer_set_blob": (_int, [_vp, _vp]),
     "zf_latent_sample": (_int, [_int, _dbl, _u64, _vp, _i64, _int, _vp]),
     "zf_flow_set_bn_stats": (_int, [_vp, _int, _vp, _vp]),
     "zf_flow_set_sb_stats": (_int, [_vp, _int, _vp, _vp]),

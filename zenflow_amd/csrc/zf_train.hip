@@ -1,0 +1,834 @@
+// Training: train-mode forward with stored activations, the reverse pass
+// (RQ spline, conditioner MLP, BatchNorm with batch statistics) and the
+// optimiser update, for zenflow.train (src/zenflow/train.py:18-138):
+//   loss_fn  (train.py:64-72): -mean(Flow.__call__(x, c, train=True))
+//   step     (train.py:80-86): jax.grad -> optax (n)adamw update
+// The path is op by op and unfused (a training batch is 10^3-10^5 rows; the
+// weights change every step, so the fused inference kernels' packed weight
+// layouts would have to be rebuilt each step).  GEMMs are an LDS-tiled fp32
+// kernel; everything else is per-row elementwise / per-column reductions.
+// All parameters and gradients live in the natural FLAX blob layout of
+// zf_flow_plan on the device.
+#include "zf_internal.h"
+#include "zf_spline.h"
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace zf {
+namespace {
+
+constexpr float kBnEps = 1e-5f;     // flax.linen.BatchNorm epsilon
+constexpr float kBnMomentum = 0.99f; // flax.linen.BatchNorm momentum
+constexpr float kEpsT = 1e-5f;       // utils.py:15
+
+__host__ __device__ __forceinline__ int pmodi(int a, int m) {
+  int r = a % m;
+  return r < 0 ? r + m : r;
+}
+
+// ---- GEMM: C[M,N] (+)= op(A)[M,K] . op(B)[K,N], row-major, fp32 -----------
+constexpr int GT = 64, GK = 16;
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                   const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                   int ldc, int accumulate) {
+  __shared__ float As[GK][GT + 1];
+  __shared__ float Bs[GK][GT + 1];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += GK) {
+    for (int e = threadIdx.x; e < GT * GK; e += 256) {
+      const int mm = TA ? (e % GT) : (e / GK), kk = TA ? (e / GT) : (e % GK);
+      const int m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < M && k < K) ? (TA ? A[(long long)k * lda + m] : A[(long long)m * lda + k]) : 0.f;
+      const int nn = TB ? (e / GK) : (e % GT), kb = TB ? (e % GK) : (e / GT);
+      const int n = n0 + nn, kq = k0 + kb;
+      Bs[kb][nn] = (n < N && kq < K) ? (TB ? B[(long long)n * ldb + kq] : B[(long long)kq * ldb + n]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GK; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + ty * 4 + i, n = n0 + tx * 4 + j;
+      if (m < M && n < N) {
+        float* c = C + (long long)m * ldc + n;
+        *c = accumulate ? *c + acc[i][j] : acc[i][j];
+      }
+    }
+}
+
+int gemm(bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
+         int ldc, bool accumulate, hipStream_t st) {
+  if (M <= 0 || N <= 0) return ZF_OK;
+  const dim3 grid((N + GT - 1) / GT, (M + GT - 1) / GT);
+  const int acc = accumulate ? 1 : 0;
+  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
+  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
+  ZF_CHECK_LAUNCH("gemm_kernel");
+  return ZF_OK;
+}
+
+inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+// ---- per-column reductions (deterministic: one thread per column) ---------
+// out[n] (+)= sum_b X[b, n] * (Y ? Y[b, n] : 1)
+__global__ void colsum_kernel(const float* __restrict__ X, const float* __restrict__ Y, int B, int N,
+                              float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const float x = X[(long long)b * N + n];
+    s += Y ? (double)x * (double)Y[(long long)b * N + n] : (double)x;
+  }
+  out[n] = accumulate ? out[n] + (float)s : (float)s;
+}
+
+// ---- ShiftBounds (train mode; bijectors.py:163-273) -------------------------
+// Natural row per dim: [mode, a, b, xmin, xmax, margin, -, -].  Batch min/max
+// of the (safe_log-transformed) column -> running xmin/xmax (:250-259).
+__global__ void sb_stats_kernel(float* __restrict__ sb, int D, const float* __restrict__ cmin,
+                                const float* __restrict__ cmax, int update) {
+  const int i = threadIdx.x;
+  if (i >= D) return;
+  float* r = sb + 8 * i;
+  if ((int)r[0] == ZF_SB_BOTH) return;
+  const float margin = r[5];
+  float lo = cmin[i], hi = cmax[i];
+  const float delta = 0.5f * (hi - lo) * margin;
+  lo = lo - delta;
+  hi = hi + delta;
+  lo = fminf(r[3], lo);  // jnp.minimum(ra_min, xmin); NaN from the batch propagates below
+  hi = fmaxf(r[4], hi);
+  if (cmin[i] != cmin[i]) lo = cmin[i];
+  if (cmax[i] != cmax[i]) hi = cmax[i];
+  if (update) { r[3] = lo; r[4] = hi; }
+  r[6] = lo;  // this step's values (used by sb_forward_kernel)
+  r[7] = hi;
+}
+
+__global__ void sb_forward_kernel(const float* __restrict__ x, float* __restrict__ y, float* __restrict__ ld,
+                                  const float* __restrict__ sb, int B, int D, int rot) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float lds = 0.f;
+  for (int i = 0; i < D; ++i) {
+    const int p = pmodi(i + rot, D);
+    const float v = x[(long long)b * D + p];
+    const float* r = sb + 8 * i;
+    const int mode = (int)r[0];
+    const float a = r[1], bb = r[2], xmin = r[6], xmax = r[7];
+    float z, l;
+    if (mode == ZF_SB_BOTH) {
+      const float mul = (float)(1.0 / ((double)bb - (double)a));
+      z = (v - a) * mul;
+      l = logf(mul);
+    } else {
+      const float mul = 1.0f / (xmax - xmin);
+      float t = v;
+      if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);
+      if (mode == ZF_SB_UPPER) t = logf((bb - v) + 1.17549435e-38f);
+      const float zr = (t - xmin) * mul;
+      z = (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);
+      l = (mode == ZF_SB_NONE) ? logf(mul) : logf(mul) - t;
+    }
+    lds = lds + l;
+    y[(long long)b * D + p] = z;
+  }
+  ld[b] = ld[b] + lds;
+}
+
+// ---- NeuralSplineCoupling pieces --------------------------------------------
+// U = hstack(xc, c): logical conditioning dim k is column pmod(dt + k + rot, D).
+__global__ void gather_u_kernel(const float* __restrict__ s, const float* __restrict__ c, float* __restrict__ U,
+                                int B, int D, int C, int dt, int dc, int rot) {
+  const int DC = dc + C;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * DC) return;
+  const long long b = i / DC;
+  const int k = (int)(i - b * DC);
+  U[i] = k < dc ? s[b * D + pmodi(dt + k + rot, D)] : c[b * C + (k - dc)];
+}
+
+// BatchNorm with batch statistics (flax, use_running_average=False):
+// mean, var = max(0, E[u^2] - E[u]^2); u_hat = (u - mean) * rsqrt(var + eps);
+// u_bn = u_hat * scale + bias.  Also the running-average update (momentum 0.99).
+__global__ void bn_stats_kernel(const double* __restrict__ csum, const double* __restrict__ csq, int B, int DC,
+                                float* __restrict__ nat_bn, float* __restrict__ mean_out,
+                                float* __restrict__ rstd_out, int update) {
+  const int k = threadIdx.x;
+  if (k >= DC) return;
+  const float mean = (float)(csum[k] / B);
+  const float mean2 = (float)(csq[k] / B);
+  const float var = fmaxf(0.f, mean2 - mean * mean);
+  mean_out[k] = mean;
+  rstd_out[k] = 1.0f / sqrtf(var + kBnEps);
+  if (update) {
+    nat_bn[k] = kBnMomentum * nat_bn[k] + (1.0f - kBnMomentum) * mean;
+    nat_bn[DC + k] = kBnMomentum * nat_bn[DC + k] + (1.0f - kBnMomentum) * var;
+  }
+}
+
+__global__ void bn_apply_kernel(const float* __restrict__ U, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ scale,
+                                const float* __restrict__ bias, float* __restrict__ Uhat, float* __restrict__ Ubn,
+                                int B, int DC) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * DC) return;
+  const int k = (int)(i % DC);
+  const float uh = (U[i] - mean[k]) * rstd[k];
+  Uhat[i] = uh;
+  Ubn[i] = uh * scale[k] + bias[k];
+}
+
+__device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+// Z += bias; H = swish(Z) (flax.linen.swish = z * sigmoid(z)).  act = 0: H = Z.
+__global__ void bias_act_kernel(float* __restrict__ Z, const float* __restrict__ bias, float* __restrict__ H,
+                                int B, int N, int act) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * N) return;
+  const float z = Z[i] + bias[i % N];
+  Z[i] = z;
+  if (act) H[i] = z * sigmoidf(z);
+}
+
+// gZ = gH * swish'(Z), swish'(z) = s + z s (1 - s)
+__global__ void swish_bwd_kernel(const float* __restrict__ gH, const float* __restrict__ Z, float* __restrict__ gZ,
+                                 long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float z = Z[i];
+  const float s = sigmoidf(z);
+  gZ[i] = gH[i] * (s + z * s * (1.0f - s));
+}
+
+__device__ __forceinline__ float sp_f(float x) { return 0.5f * (x + sqrtf(x * x + 4.0f)); }
+__device__ __forceinline__ float sp_grad(float x) { return 0.5f * (1.0f + x / sqrtf(x * x + 4.0f)); }
+
+constexpr int kMaxK = 64;
+
+// One (row, transformed dim): normalize_spline_params (utils.py:37-62) of the
+// raw conditioner outputs p[0..3K-1), bin, RQ spline forward (utils.py:65-141).
+// With grads: reverse pass for gy (dL/dy) and gl (dL/dlog_det): dL/dx and dL/dp.
+template <bool GRAD>
+__device__ void spline_row(const float* __restrict__ p, int K, float x, float& y, float& ld, float gy, float gl,
+                           float* gx, float* __restrict__ gp) {
+  const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // utils.py:32-34, Python floats
+  const float cc = (float)c64, norm = (float)(1.0 + c64 * (double)K);
+  float w[kMaxK], h[kMaxK], sa[kMaxK], sb[kMaxK];
+  float Sa = 0.f, Sb = 0.f;
+  for (int j = 0; j < K; ++j) {
+    sa[j] = sp_f(p[j]);
+    sb[j] = sp_f(p[K + j]);
+    Sa = Sa + sa[j];
+    Sb = Sb + sb[j];
+  }
+  for (int j = 0; j < K; ++j) {
+    w[j] = (sa[j] / Sa + cc) / norm;
+    h[j] = (sb[j] / Sb + cc) / norm;
+  }
+  // bin: count semantics of _index (utils.py:244-250)
+  float xk = 0.f, yk = 0.f;
+  int cnt = 0;
+  {
+    float t = 0.f;
+    for (int j = 0; j <= K; ++j) {
+      if (t <= x) ++cnt;
+      if (j < K) t = t + w[j];
+    }
+  }
+  int idx = cnt - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  for (int j = 0; j < idx; ++j) { xk = xk + w[j]; yk = yk + h[j]; }
+  const bool oob = (x < 0.f) || (x >= 1.f);
+  if (idx == K || oob) {
+    // idx == K: the reference's fill-mode gather gives NaN (utils.py:224-230);
+    // oob rows are the identity with log_det 0 (:130, :138).
+    y = oob ? x : __builtin_nanf("");
+    ld = oob ? 0.f : __builtin_nanf("");
+    if (GRAD) {
+      *gx = oob ? gy : __builtin_nanf("");
+      for (int j = 0; j < 3 * K - 1; ++j) gp[j] = 0.f;
+    }
+    return;
+  }
+  const float wk = w[idx], hk = h[idx];
+  const float dk = (idx == 0) ? 1.f : sp_f(p[2 * K + idx - 1]);
+  const float dk1 = (idx + 1 == K) ? 1.f : sp_f(p[2 * K + idx]);
+  const float sk = hk / wk;
+  const float zr = (x - xk) / wk;
+  const float z = fminf(fmaxf(zr, kEpsT), 0.99999f);
+  const float az = 1.0f - z;
+  const float num = hk * z * (sk * z + dk * az);
+  const float den = sk + (dk1 + dk - 2.0f * sk) * z * az;
+  y = yk + num / (den + kEpsT);
+  const float q = z * (dk1 * z + 2.0f * sk * az) + dk * (az * az);
+  ld = 2.0f * logf(sk + kEpsT) + logf(q + kEpsT) - 2.0f * logf(den + kEpsT);
+  if (!GRAD) return;
+  // ---- reverse pass ----
+  const float dE = den + kEpsT;
+  float g_yk = gy;
+  const float g_num = gy / dE;
+  float g_den = -gy * num / (dE * dE) - 2.0f * gl / dE;
+  float g_sk = 2.0f * gl / (sk + kEpsT);
+  const float g_q = gl / (q + kEpsT);
+  float g_hk = g_num * (sk * z * z + dk * z * az);
+  g_sk += g_num * hk * z * z;
+  float g_dk = g_num * hk * z * az;
+  float g_z = g_num * hk * (2.0f * sk * z + dk * (az - z));
+  g_sk += g_den * (1.0f - 2.0f * z * az);
+  float g_dk1 = g_den * z * az;
+  g_dk += g_den * z * az;
+  g_z += g_den * (dk1 + dk - 2.0f * sk) * (az - z);
+  g_dk1 += g_q * z * z;
+  g_sk += g_q * 2.0f * z * az;
+  g_dk += g_q * az * az;
+  g_z += g_q * (2.0f * dk1 * z + 2.0f * sk * (az - z) - 2.0f * dk * az);
+  const float g_zr = (zr > kEpsT && zr < 0.99999f) ? g_z : 0.f;  // jnp.clip passes inside only
+  *gx = g_zr / wk;
+  const float g_xk = -g_zr / wk;
+  float g_wk = -g_zr * zr / wk;
+  g_hk += g_sk / wk;
+  g_wk += -g_sk * hk / (wk * wk);
+  // scatter to widths / heights: xk = sum_{j<idx} w_j, yk likewise
+  float gw[kMaxK], gh[kMaxK];
+  for (int j = 0; j < K; ++j) {
+    gw[j] = (j < idx) ? g_xk : 0.f;
+    gh[j] = (j < idx) ? g_yk : 0.f;
+  }
+  gw[idx] += g_wk;
+  gh[idx] += g_hk;
+  // normalisation: w_j = (sa_j / Sa + c) / norm
+  float tw = 0.f, th = 0.f;
+  for (int j = 0; j < K; ++j) { tw += gw[j] * sa[j]; th += gh[j] * sb[j]; }
+  for (int j = 0; j < K; ++j) {
+    const float gsa = (gw[j] / Sa - tw / (Sa * Sa)) / norm;
+    const float gsb = (gh[j] / Sb - th / (Sb * Sb)) / norm;
+    gp[j] = gsa * sp_grad(p[j]);
+    gp[K + j] = gsb * sp_grad(p[K + j]);
+  }
+  for (int j = 0; j < K - 1; ++j) gp[2 * K + j] = 0.f;
+  if (idx >= 1) gp[2 * K + idx - 1] += g_dk * sp_grad(p[2 * K + idx - 1]);
+  if (idx + 1 < K) gp[2 * K + idx] += g_dk1 * sp_grad(p[2 * K + idx]);
+}
+
+// Forward: transformed dims (logical d < dt at column pmod(d + rot, D)) through
+// the spline; conditioning columns copied; log-det summed in dim order.
+__global__ void spline_fwd_kernel(const float* __restrict__ s_in, float* __restrict__ s_out,
+                                  const float* __restrict__ P, float* __restrict__ ld, int B, int D, int dt, int K,
+                                  int rot) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int S = 3 * K - 1;
+  for (int j = 0; j < D; ++j) s_out[(long long)b * D + j] = s_in[(long long)b * D + j];
+  float l = 0.f;
+  for (int d = 0; d < dt; ++d) {
+    const int col = pmodi(d + rot, D);
+    float y, ldv;
+    spline_row<false>(P + ((long long)b * dt + d) * S, K, s_in[(long long)b * D + col], y, ldv, 0.f, 0.f, nullptr,
+                      nullptr);
+    s_out[(long long)b * D + col] = y;
+    l = l + ldv;
+  }
+  ld[b] = ld[b] + l;
+}
+
+// Reverse: g_in = dL/d(state_in) from g_out = dL/d(state_out) and gl per row;
+// conditioning columns pass g_out through (their MLP share is added later).
+__global__ void spline_bwd_kernel(const float* __restrict__ s_in, const float* __restrict__ P,
+                                  const float* __restrict__ g_out, float gl, float* __restrict__ g_in,
+                                  float* __restrict__ gP, int B, int D, int dt, int K, int rot) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int S = 3 * K - 1;
+  for (int j = 0; j < D; ++j) g_in[(long long)b * D + j] = g_out[(long long)b * D + j];
+  for (int d = 0; d < dt; ++d) {
+    const int col = pmodi(d + rot, D);
+    float y, ldv, gx;
+    spline_row<true>(P + ((long long)b * dt + d) * S, K, s_in[(long long)b * D + col], y, ldv,
+                     g_out[(long long)b * D + col], gl, &gx, gP + ((long long)b * dt + d) * S);
+    g_in[(long long)b * D + col] = gx;
+  }
+}
+
+// BatchNorm reverse with batch statistics:
+// gU = rstd * (gUhat - mean(gUhat) - u_hat * mean(gUhat * u_hat)), gUhat = gUbn * scale.
+__global__ void bn_bwd_kernel(const float* __restrict__ gUbn, const float* __restrict__ Uhat,
+                              const float* __restrict__ scale, const float* __restrict__ rstd,
+                              const float* __restrict__ sum_g, const float* __restrict__ sum_gu,
+                              float* __restrict__ gU, int B, int DC) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * DC) return;
+  const int k = (int)(i % DC);
+  // sum_g / sum_gu are sums of gUbn and gUbn*Uhat; scale them into gUhat terms
+  const float mg = scale[k] * sum_g[k] / B, mgu = scale[k] * sum_gu[k] / B;
+  gU[i] = rstd[k] * (gUbn[i] * scale[k] - mg - Uhat[i] * mgu);
+}
+
+__global__ void scatter_gu_kernel(const float* __restrict__ gU, float* __restrict__ g, int B, int D, int C, int dt,
+                                  int dc, int rot) {
+  const int DC = dc + C;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * dc) return;
+  const long long b = i / dc;
+  const int k = (int)(i - b * dc);
+  g[b * D + pmodi(dt + k + rot, D)] += gU[b * DC + k];
+}
+
+// ---- latent + loss ------------------------------------------------------------
+// lp = latent.log_prob(z) + log_det, nan_to_num (flow.py:45-47); loss partials
+// -lp/B (fp64); gz = -(1/B) d latent_lp / dz (zero where lp is not finite).
+__global__ void latent_loss_kernel(const float* __restrict__ z, const float* __restrict__ ld, int B, int D, int rot,
+                                   int latent, float a, float betac, float tnmass, float* __restrict__ gz,
+                                   double* __restrict__ partial) {
+  __shared__ double sm[256];
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  double contrib = 0.0;
+  if (b < B) {
+    float lat = 0.f;
+    for (int j = 0; j < D; ++j) {
+      const float v = z[(long long)b * D + pmodi(j + rot, D)];
+      float t;
+      if (latent == ZF_LATENT_NORMAL || latent == ZF_LATENT_TRUNCNORM) {
+        const float dv = v - 0.5f;
+        t = (logf(6.28318530717958647692f * 0.01f) + (dv * dv) / 0.01f) / -2.0f;
+        if (latent == ZF_LATENT_TRUNCNORM) {
+          t = t - tnmass;
+          if (dv / 0.1f < -5.f || dv / 0.1f > 5.f) t = -INFINITY;
+        }
+      } else if (latent == ZF_LATENT_BETA) {
+        const float am1 = a - 1.0f;
+        t = betac + (am1 == 0.f ? 0.f : am1 * logf(v)) + (am1 == 0.f ? 0.f : am1 * log1pf(-v));
+        if (v > 1.f || v < 0.f) t = -INFINITY;
+      } else {
+        t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
+      }
+      lat = lat + t;
+    }
+    float lp = lat + ld[b];
+    const bool fin = (lp == lp) && lp != INFINITY && lp != -INFINITY;
+    if (lp != lp) lp = -INFINITY;
+    if (lp == INFINITY) lp = 3.40282347e38f;
+    if (lp == -INFINITY) lp = -3.40282347e38f;
+    contrib = -(double)lp / B;
+    const float s = -1.0f / B;
+    for (int j = 0; j < D; ++j) {
+      const int col = pmodi(j + rot, D);
+      const float v = z[(long long)b * D + col];
+      float g = 0.f;
+      if (fin) {
+        if (latent == ZF_LATENT_NORMAL || latent == ZF_LATENT_TRUNCNORM) g = -(v - 0.5f) / 0.01f;
+        else if (latent == ZF_LATENT_BETA) g = (a - 1.0f) / v - (a - 1.0f) / (1.0f - v);
+      }
+      gz[(long long)b * D + col] = s * g;
+    }
+  }
+  sm[threadIdx.x] = contrib;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if ((int)threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sm[0];
+}
+
+__global__ void sum_partials_kernel(const double* __restrict__ part, int n, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += part[i];
+  out[0] = s;
+}
+
+// ---- optimiser: optax adamw / nadamw ---------------------------------------
+// scale_by_adam(b1, b2, eps, nesterov) -> add_decayed_weights(wd) -> scale(-lr)
+// (optax/_src/transform.py, alias.py), masked to the parameter entries.
+__global__ void adam_kernel(float* __restrict__ prm, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, const unsigned char* __restrict__ mask, long long n, float lr,
+                            float b1, float b2, float eps, float wd, int nesterov, float bc1, float bc1n,
+                            float bc2) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !mask[i]) return;
+  const float gi = g[i];
+  const float mi = b1 * m[i] + (1.0f - b1) * gi;
+  const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  // bias corrections: bc1 = 1 - b1^t, bc1n = 1 - b1^(t+1), bc2 = 1 - b2^t
+  const float mhat = nesterov ? b1 * (mi / bc1n) + (1.0f - b1) * (gi / bc1) : mi / bc1;
+  const float vhat = vi / bc2;
+  const float upd = mhat / (sqrtf(vhat) + eps) + wd * prm[i];
+  prm[i] = prm[i] - lr * upd;
+}
+
+}  // namespace
+}  // namespace zf
+
+// ============================================================================
+struct zf_trainer {
+  zf_flow_desc desc;
+  int D = 0, C = 0, n_ops = 0;
+  int64_t nat_floats = 0;
+  int64_t bmax = 0;
+  zf_optim_desc opt;
+  long long t = 0;  // optimiser step count
+  std::vector<float> sb_modes, sb_prm;  // ShiftBounds pre-transform per dim (colstats)
+  float* d_nat = nullptr;
+  float* d_grad = nullptr;
+  float* d_m = nullptr;
+  float* d_v = nullptr;
+  unsigned char* d_mask = nullptr;
+  // arena: per-op saved activations + scratch
+  std::vector<float*> bufs;
+  std::vector<int64_t> sizes;
+  float* d_state = nullptr;   // [n_ops + 1][bmax][D] states before each op
+  float* d_ld = nullptr;      // [bmax]
+  float* d_g0 = nullptr;      // [bmax][D]
+  float* d_g1 = nullptr;
+  float* d_small = nullptr;   // per-column scratch
+  double* d_dsmall = nullptr;
+  double* d_part = nullptr;
+  void* d_colws = nullptr;
+  int64_t colws_bytes = 0;
+  struct NscBufs {
+    float *U, *Uhat, *Ubn, *P, *gP, *gU, *gA, *gB;
+    std::vector<float*> Z, H;
+    float *mean, *rstd;
+  };
+  std::vector<NscBufs> nsc;
+};
+
+namespace zf {
+namespace {
+
+float* dmalloc(zf_trainer* t, int64_t n, int& rc) {
+  if (rc) return nullptr;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, (size_t)(n > 0 ? n : 1) * sizeof(float));
+  if (e != hipSuccess) {
+    rc = hip_status(e, "zf_trainer alloc");
+    return nullptr;
+  }
+  t->bufs.push_back((float*)p);
+  return (float*)p;
+}
+
+int nsc_dims(const zf_trainer* t, const zf_op_desc& op, int& dt, int& dc, int& DC, int& S) {
+  dt = t->D / 2;
+  dc = t->D - dt;
+  DC = dc + t->C;
+  S = 3 * op.knots - 1;
+  return ZF_OK;
+}
+
+}  // namespace
+}  // namespace zf
+
+extern "C" {
+
+int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t blob_floats,
+                      const unsigned char* param_mask, int64_t batch_max, const zf_optim_desc* opt,
+                      zf_trainer_t** out) {
+  if (!desc_in || !blob_host || !param_mask || !opt || !out) return zf::einval("NULL argument");
+  *out = nullptr;
+  zf_flow_desc desc = *desc_in;
+  int64_t need = 0;
+  int rc = zf_flow_plan(&desc, &need);
+  if (rc) return rc;
+  if (need != blob_floats) return zf::einval("blob has %lld floats, plan needs %lld", (long long)blob_floats, (long long)need);
+  if (batch_max < 1) return zf::einval("batch_max < 1");
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind == ZF_OP_SHIFT_BOUNDS && i != 0)
+      return zf::enotsup("training: ShiftBounds is supported only as the first bijector");
+    if (op.kind == ZF_OP_NSC && op.knots > zf::kMaxK) return zf::enotsup("training: knots > 64");
+    if (op.kind == ZF_OP_NSC && desc.dim - desc.dim / 2 + desc.cond_dim > 64)
+      return zf::enotsup("training: more than 64 conditioner inputs");
+  }
+  zf_trainer* t = new zf_trainer();
+  t->desc = desc;
+  t->D = desc.dim;
+  t->C = desc.cond_dim;
+  t->n_ops = desc.n_ops;
+  t->nat_floats = need;
+  t->bmax = batch_max;
+  t->opt = *opt;
+  const int64_t B = batch_max, D = desc.dim;
+  if (desc.n_ops > 0 && desc.ops[0].kind == ZF_OP_SHIFT_BOUNDS) {
+    const float* row = blob_host + desc.ops[0].off_sb;
+    for (int j = 0; j < D; ++j) {
+      const int mode = (int)row[8 * j];
+      t->sb_modes.push_back((float)mode);
+      t->sb_prm.push_back(mode == ZF_SB_LOWER ? row[8 * j + 1] : row[8 * j + 2]);
+    }
+  }
+  rc = ZF_OK;
+  t->d_nat = zf::dmalloc(t, need, rc);
+  t->d_grad = zf::dmalloc(t, need, rc);
+  t->d_m = zf::dmalloc(t, need, rc);
+  t->d_v = zf::dmalloc(t, need, rc);
+  t->d_mask = (unsigned char*)zf::dmalloc(t, (need + 3) / 4, rc);
+  t->d_state = zf::dmalloc(t, (int64_t)(desc.n_ops + 1) * B * D, rc);
+  t->d_ld = zf::dmalloc(t, B, rc);
+  t->d_g0 = zf::dmalloc(t, B * D, rc);
+  t->d_g1 = zf::dmalloc(t, B * D, rc);
+  t->d_small = zf::dmalloc(t, 8 * 256, rc);
+  t->d_dsmall = (double*)zf::dmalloc(t, 4 * 256, rc);
+  t->d_part = (double*)zf::dmalloc(t, 2 * ((B + 255) / 256 + 1), rc);
+  t->colws_bytes = zf_colstats_workspace_bytes(B, 64);
+  t->d_colws = zf::dmalloc(t, t->colws_bytes / 4 + 1, rc);
+  t->nsc.resize(desc.n_ops);
+  for (int i = 0; i < desc.n_ops && !rc; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    int dt, dc, DC, S;
+    zf::nsc_dims(t, op, dt, dc, DC, S);
+    zf_trainer::NscBufs& nb = t->nsc[i];
+    nb.U = zf::dmalloc(t, B * DC, rc);
+    nb.Uhat = zf::dmalloc(t, B * DC, rc);
+    nb.Ubn = zf::dmalloc(t, B * DC, rc);
+    nb.gU = zf::dmalloc(t, B * DC, rc);
+    nb.P = zf::dmalloc(t, B * dt * S, rc);
+    nb.gP = zf::dmalloc(t, B * dt * S, rc);
+    int hmax = 0;
+    for (int l = 0; l < op.n_hidden; ++l) {
+      nb.Z.push_back(zf::dmalloc(t, B * op.hidden[l], rc));
+      nb.H.push_back(zf::dmalloc(t, B * op.hidden[l], rc));
+      hmax = op.hidden[l] > hmax ? op.hidden[l] : hmax;
+    }
+    nb.gA = zf::dmalloc(t, B * hmax, rc);
+    nb.gB = zf::dmalloc(t, B * hmax, rc);
+    nb.mean = zf::dmalloc(t, DC, rc);
+    nb.rstd = zf::dmalloc(t, DC, rc);
+  }
+  hipError_t e = hipSuccess;
+  if (!rc) e = hipMemcpy(t->d_nat, blob_host, need * sizeof(float), hipMemcpyHostToDevice);
+  if (!rc && e == hipSuccess) e = hipMemcpy(t->d_mask, param_mask, need, hipMemcpyHostToDevice);
+  if (!rc && e == hipSuccess) e = hipMemset(t->d_m, 0, need * sizeof(float));
+  if (!rc && e == hipSuccess) e = hipMemset(t->d_v, 0, need * sizeof(float));
+  if (!rc && e != hipSuccess) rc = zf::hip_status(e, "zf_trainer_create");
+  if (rc) {
+    zf_trainer_destroy(t);
+    return rc;
+  }
+  *out = t;
+  return ZF_OK;
+}
+
+int zf_trainer_destroy(zf_trainer_t* t) {
+  if (!t) return ZF_OK;
+  for (float* p : t->bufs) (void)hipFree(p);
+  delete t;
+  return ZF_OK;
+}
+
+int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_t B64, int update_stats,
+                         double* loss, float* grad, void* stream) {
+  if (!t) return zf::einval("trainer is NULL");
+  if (B64 < 1 || B64 > t->bmax) return zf::einval("batch %lld outside [1, %lld]", (long long)B64, (long long)t->bmax);
+  if (!x) return zf::einval("x is NULL");
+  if (t->C > 0 && !c) return zf::einval("flow is conditional but c is NULL");
+  hipStream_t st = (hipStream_t)stream;
+  const int B = (int)B64, D = t->D, C = t->C;
+  const zf_flow_desc& desc = t->desc;
+  float* nat = t->d_nat;
+  auto state = [&](int i) { return t->d_state + (int64_t)i * t->bmax * D; };
+  ZF_TRY_HIP(hipMemcpyAsync(state(0), x, (size_t)B * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+  ZF_TRY_HIP(hipMemsetAsync(t->d_ld, 0, (size_t)B * sizeof(float), st));
+  int rc;
+  // ---- forward (train mode) ----
+  int rot = 0;
+  std::vector<int> rots(desc.n_ops + 1, 0);
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    rots[i] = rot;
+    float* sin = state(i);
+    float* sout = state(i + 1);
+    if (op.kind == ZF_OP_ROLL) {
+      ZF_TRY_HIP(hipMemcpyAsync(sout, sin, (size_t)B * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+      rot = zf::pmodi(rot - op.shift, D);
+    } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
+      float* sb = nat + op.off_sb;
+      // batch min / max of the (safe_log-transformed) columns (first op: rot == 0)
+      rc = zf_colstats(sin, B, D, D, 0, t->sb_modes.data(), t->sb_prm.data(), t->d_small, t->d_small + 64,
+                       nullptr, nullptr, t->d_colws, stream);
+      if (rc) return rc;
+      hipLaunchKernelGGL(zf::sb_stats_kernel, dim3(1), dim3(64), 0, st, sb, D, t->d_small, t->d_small + 64,
+                         update_stats);
+      ZF_CHECK_LAUNCH("sb_stats_kernel");
+      hipLaunchKernelGGL(zf::sb_forward_kernel, dim3(zf::blocks_for(B)), dim3(256), 0, st, sin, sout, t->d_ld, sb, B,
+                         D, rot);
+      ZF_CHECK_LAUNCH("sb_forward_kernel");
+    } else if (op.kind == ZF_OP_NSC) {
+      int dt, dc, DC, S;
+      zf::nsc_dims(t, op, dt, dc, DC, S);
+      zf_trainer::NscBufs& nb = t->nsc[i];
+      hipLaunchKernelGGL(zf::gather_u_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, sin, c, nb.U,
+                         B, D, C, dt, dc, rot);
+      ZF_CHECK_LAUNCH("gather_u_kernel");
+      rc = zf_colstats(nb.U, B, DC, DC, 0, nullptr, nullptr, nullptr, nullptr, t->d_dsmall, t->d_dsmall + 128,
+                       t->d_colws, stream);
+      if (rc) return rc;
+      float* bn = nat + op.off_bn;  // [mean, var, scale, bias]
+      hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(128), 0, st, t->d_dsmall, t->d_dsmall + 128, B, DC, bn,
+                         nb.mean, nb.rstd, update_stats);
+      ZF_CHECK_LAUNCH("bn_stats_kernel");
+      hipLaunchKernelGGL(zf::bn_apply_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.U, nb.mean,
+                         nb.rstd, bn + 2 * DC, bn + 3 * DC, nb.Uhat, nb.Ubn, B, DC);
+      ZF_CHECK_LAUNCH("bn_apply_kernel");
+      const float* in = nb.Ubn;
+      int in_w = DC;
+      for (int l = 0; l <= op.n_hidden; ++l) {
+        const bool last = (l == op.n_hidden);
+        const int out_w = last ? dt * S : op.hidden[l];
+        float* Z = last ? nb.P : nb.Z[l];
+        rc = zf::gemm(false, false, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, false, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(zf::bias_act_kernel, dim3(zf::blocks_for((int64_t)B * out_w)), dim3(256), 0, st, Z,
+                           nat + op.off_b[l], last ? nullptr : nb.H[l], B, out_w, last ? 0 : 1);
+        ZF_CHECK_LAUNCH("bias_act_kernel");
+        if (!last) {
+          in = nb.H[l];
+          in_w = out_w;
+        }
+      }
+      hipLaunchKernelGGL(zf::spline_fwd_kernel, dim3(zf::blocks_for(B, 64)), dim3(64), 0, st, sin, sout, nb.P,
+                         t->d_ld, B, D, dt, op.knots, rot);
+      ZF_CHECK_LAUNCH("spline_fwd_kernel");
+    } else {
+      return zf::einval("op %d: unknown kind", i);
+    }
+  }
+  rots[desc.n_ops] = rot;
+  // ---- latent + loss ----
+  const int lt = desc.latent;
+  const float a = (float)desc.latent_param;
+  const float betac = lt == ZF_LATENT_BETA
+                          ? (float)(-(std::lgamma(desc.latent_param) * 2.0 - std::lgamma(2.0 * desc.latent_param)))
+                          : 0.f;
+  const float tnm = (float)std::log1p(-2.0 * 0.5 * std::erfc(5.0 / std::sqrt(2.0)));
+  const int nblk = (int)zf::blocks_for(B);
+  float* g = t->d_g0;
+  float* g_prev = t->d_g1;
+  hipLaunchKernelGGL(zf::latent_loss_kernel, dim3(nblk), dim3(256), 0, st, state(desc.n_ops), t->d_ld, B, D, rot, lt,
+                     a, betac, tnm, g, t->d_part);
+  ZF_CHECK_LAUNCH("latent_loss_kernel");
+  hipLaunchKernelGGL(zf::sum_partials_kernel, dim3(1), dim3(64), 0, st, t->d_part, nblk, t->d_part + nblk);
+  ZF_CHECK_LAUNCH("sum_partials_kernel");
+  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, t->d_part + nblk, sizeof(double), hipMemcpyDeviceToDevice, st));
+  // ---- reverse ----
+  float* G = grad ? grad : t->d_grad;
+  ZF_TRY_HIP(hipMemsetAsync(G, 0, (size_t)t->nat_floats * sizeof(float), st));
+  const float gl = -1.0f / (float)B;  // d loss / d log_det of every op and row
+  for (int i = desc.n_ops - 1; i >= 0; --i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind == ZF_OP_ROLL || op.kind == ZF_OP_SHIFT_BOUNDS) continue;  // Roll: index map; SB: first op
+    int dt, dc, DC, S;
+    zf::nsc_dims(t, op, dt, dc, DC, S);
+    zf_trainer::NscBufs& nb = t->nsc[i];
+    const int r = rots[i];
+    // spline: g -> g_prev (transformed columns), gP
+    hipLaunchKernelGGL(zf::spline_bwd_kernel, dim3(zf::blocks_for(B, 64)), dim3(64), 0, st, state(i), nb.P, g, gl,
+                       g_prev, nb.gP, B, D, dt, op.knots, r);
+    ZF_CHECK_LAUNCH("spline_bwd_kernel");
+    // MLP reverse
+    const float* gout = nb.gP;
+    int out_w = dt * S;
+    float* gbufs[2] = {nb.gA, nb.gB};
+    int which = 0;
+    for (int l = op.n_hidden; l >= 0; --l) {
+      const int in_w = l == 0 ? DC : op.hidden[l - 1];
+      const float* hin = l == 0 ? nb.Ubn : nb.H[l - 1];
+      // dW_l = hin^T . gout ; db_l = colsum(gout)
+      rc = zf::gemm(true, false, in_w, out_w, B, hin, in_w, gout, out_w, G + op.off_w[l], out_w, false, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL(zf::colsum_kernel, dim3(zf::blocks_for(out_w, 128)), dim3(128), 0, st, gout, nullptr, B,
+                         out_w, G + op.off_b[l], 0);
+      ZF_CHECK_LAUNCH("colsum_kernel");
+      // g_in = gout . W_l^T
+      float* gin = l == 0 ? nb.gU : gbufs[which];
+      rc = zf::gemm(false, true, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, false, st);
+      if (rc) return rc;
+      if (l > 0) {  // through swish of layer l-1
+        hipLaunchKernelGGL(zf::swish_bwd_kernel, dim3(zf::blocks_for((int64_t)B * in_w)), dim3(256), 0, st, gin,
+                           nb.Z[l - 1], gin, (long long)B * in_w);
+        ZF_CHECK_LAUNCH("swish_bwd_kernel");
+        gout = gin;
+        out_w = in_w;
+        which ^= 1;
+      }
+    }
+    // BatchNorm: gU holds d loss / d Ubn
+    float* bn = nat + op.off_bn;
+    float* gbn = G + op.off_bn;
+    hipLaunchKernelGGL(zf::colsum_kernel, dim3(1), dim3(128), 0, st, nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, 0);
+    ZF_CHECK_LAUNCH("colsum_kernel");
+    hipLaunchKernelGGL(zf::colsum_kernel, dim3(1), dim3(128), 0, st, nb.gU, nullptr, B, DC, gbn + 3 * DC, 0);
+    ZF_CHECK_LAUNCH("colsum_kernel");
+    // gU := d loss / d U, in place (reads each element before writing it)
+    hipLaunchKernelGGL(zf::bn_bwd_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.gU, nb.Uhat,
+                       bn + 2 * DC, nb.rstd, gbn + 3 * DC, gbn + 2 * DC, nb.gU, B, DC);
+    ZF_CHECK_LAUNCH("bn_bwd_kernel");
+    hipLaunchKernelGGL(zf::scatter_gu_kernel, dim3(zf::blocks_for((int64_t)B * dc)), dim3(256), 0, st, nb.gU, g_prev,
+                       B, D, C, dt, dc, r);
+    ZF_CHECK_LAUNCH("scatter_gu_kernel");
+    float* tmp = g;
+    g = g_prev;
+    g_prev = tmp;
+  }
+  return ZF_OK;
+}
+
+int zf_trainer_step(zf_trainer_t* t, const float* x, const float* c, int64_t B, double* loss, void* stream) {
+  if (!t) return zf::einval("trainer is NULL");
+  int rc = zf_trainer_loss_grad(t, x, c, B, 1, loss, nullptr, stream);
+  if (rc) return rc;
+  t->t += 1;
+  const zf_optim_desc& o = t->opt;
+  const double tt = (double)t->t;
+  const float bc1 = (float)(1.0 - std::pow((double)o.b1, tt));
+  const float bc1n = (float)(1.0 - std::pow((double)o.b1, tt + 1.0));
+  const float bc2 = (float)(1.0 - std::pow((double)o.b2, tt));
+  hipLaunchKernelGGL(zf::adam_kernel, dim3(zf::blocks_for(t->nat_floats)), dim3(256), 0, (hipStream_t)stream,
+                     t->d_nat, t->d_grad, t->d_m, t->d_v, t->d_mask, (long long)t->nat_floats, o.learning_rate, o.b1,
+                     o.b2, o.eps, o.weight_decay, o.nesterov, bc1, bc1n, bc2);
+  ZF_CHECK_LAUNCH("adam_kernel");
+  return ZF_OK;
+}
+
+int zf_trainer_get_blob(zf_trainer_t* t, float* blob_host) {
+  if (!t || !blob_host) return zf::einval("NULL argument");
+  ZF_TRY_HIP(hipDeviceSynchronize());
+  ZF_TRY_HIP(hipMemcpy(blob_host, t->d_nat, t->nat_floats * sizeof(float), hipMemcpyDeviceToHost));
+  return ZF_OK;
+}
+
+int zf_trainer_set_blob(zf_trainer_t* t, const float* blob_host) {
+  if (!t || !blob_host) return zf::einval("NULL argument");
+  ZF_TRY_HIP(hipDeviceSynchronize());
+  ZF_TRY_HIP(hipMemcpy(t->d_nat, blob_host, t->nat_floats * sizeof(float), hipMemcpyHostToDevice));
+  return ZF_OK;
+}
+
+}  // extern "C"

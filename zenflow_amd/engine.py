@@ -124,7 +124,9 @@ class Program:
         lib = L.load_library()
         check(lib.zf_flow_plan(ct.byref(desc), ct.byref(n)), "zf_flow_plan")
         blob = np.zeros(max(1, n.value), np.float32)
+        self.param_mask = np.zeros(blob.shape, np.uint8)
         self._fill_blob(desc, blob, params, stats)
+        self.blob = blob  # natural layout (host copy): what the trainer starts from
         h = ct.c_void_p()
         check(lib.zf_flow_create(ct.byref(desc), blob.ctypes.data, n.value, ct.byref(h)), "zf_flow_create")
         self.desc = desc
@@ -153,7 +155,7 @@ class Program:
                 for j, (mode, a, b) in enumerate(sb_modes(op.module, D)):
                     xmin = np.asarray(st.get(f"xmin_{j}", [np.inf]), np.float32).reshape(-1)[0]
                     xmax = np.asarray(st.get(f"xmax_{j}", [-np.inf]), np.float32).reshape(-1)[0]
-                    blob[d.off_sb + 8 * j : d.off_sb + 8 * j + 5] = [mode, a, b, xmin, xmax]
+                    blob[d.off_sb + 8 * j : d.off_sb + 8 * j + 6] = [mode, a, b, xmin, xmax, op.module.margin]
             elif op.kind == L.ZF_OP_NSC:
                 p = get_path(params, op.path)
                 s = get_path(stats, op.path)
@@ -168,6 +170,7 @@ class Program:
                 blob[o + DC : o + 2 * DC] = _arr(bns.get("var", np.ones(DC)), (DC,), "BatchNorm_0/var")
                 blob[o + 2 * DC : o + 3 * DC] = _arr(bnp.get("scale", np.ones(DC)), (DC,), "BatchNorm_0/scale")
                 blob[o + 3 * DC : o + 4 * DC] = _arr(bnp.get("bias", np.zeros(DC)), (DC,), "BatchNorm_0/bias")
+                self.param_mask[o + 2 * DC : o + 4 * DC] = 1
                 widths = list(op.module.layers) + [dt * (3 * op.module.knots - 1)]
                 fan_in = DC
                 for l, w in enumerate(widths):
@@ -178,7 +181,42 @@ class Program:
                     b = _arr(dense["bias"], (w,), f"Dense_{l}/bias")
                     blob[d.off_w[l] : d.off_w[l] + k.size] = k.ravel()
                     blob[d.off_b[l] : d.off_b[l] + w] = b
+                    self.param_mask[d.off_w[l] : d.off_w[l] + k.size] = 1
+                    self.param_mask[d.off_b[l] : d.off_b[l] + w] = 1
                     fan_in = w
+
+    def blob_to_variables(self, blob: np.ndarray) -> Dict[str, Any]:
+        """Inverse of _fill_blob: {"params": ..., "batch_stats": ...} of the
+        bijector (FLAX layout) from a natural blob."""
+        D, Cd = self.D, self.C
+        params: Dict[str, Any] = {}
+        stats: Dict[str, Any] = {}
+        f32 = np.float32
+        for i, op in enumerate(self.ops):
+            d = self.desc.ops[i]
+            if op.kind == L.ZF_OP_SHIFT_BOUNDS:
+                for j, (mode, _, _) in enumerate(sb_modes(op.module, D)):
+                    if mode == L.ZF_SB_BOTH:
+                        continue
+                    r = d.off_sb + 8 * j
+                    set_path(stats, op.path + (f"xmin_{j}",), np.array([blob[r + 3]], f32))
+                    set_path(stats, op.path + (f"xmax_{j}",), np.array([blob[r + 4]], f32))
+            elif op.kind == L.ZF_OP_NSC:
+                dt = D // 2
+                DC = D - dt + Cd
+                o = d.off_bn
+                set_path(stats, op.path + ("BatchNorm_0", "mean"), blob[o : o + DC].astype(f32).copy())
+                set_path(stats, op.path + ("BatchNorm_0", "var"), blob[o + DC : o + 2 * DC].astype(f32).copy())
+                set_path(params, op.path + ("BatchNorm_0", "scale"), blob[o + 2 * DC : o + 3 * DC].astype(f32).copy())
+                set_path(params, op.path + ("BatchNorm_0", "bias"), blob[o + 3 * DC : o + 4 * DC].astype(f32).copy())
+                widths = list(op.module.layers) + [dt * (3 * op.module.knots - 1)]
+                fan_in = DC
+                for l, w in enumerate(widths):
+                    k = blob[d.off_w[l] : d.off_w[l] + fan_in * w].reshape(fan_in, w).astype(f32).copy()
+                    set_path(params, op.path + (f"Dense_{l}", "kernel"), k)
+                    set_path(params, op.path + (f"Dense_{l}", "bias"), blob[d.off_b[l] : d.off_b[l] + w].astype(f32).copy())
+                    fan_in = w
+        return {"params": params, "batch_stats": stats}
 
     # -- helpers ---------------------------------------------------------------
     def workspace(self, N: int) -> DeviceArray:
