@@ -12,12 +12,15 @@
 #include "zf_internal.h"
 #include "zf_spline.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
 
 namespace zf {
 namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr float kBnEps = 1e-5f;     // flax.linen.BatchNorm epsilon
 constexpr float kBnMomentum = 0.99f; // flax.linen.BatchNorm momentum
@@ -28,81 +31,255 @@ __host__ __device__ __forceinline__ int pmodi(int a, int m) {
   return r < 0 ? r + m : r;
 }
 
-// ---- GEMM: C[M,N] (+)= op(A)[M,K] . op(B)[K,N], row-major, fp32 -----------
-constexpr int GT = 64, GK = 16;
+// ---- GEMM on fp32 MFMA: C[M,N] = op(A)[M,K] . op(B)[K,N], row-major ----------
+// v_mfma_f32_32x32x2_f32 is a k-ordered f32 fma chain (exact f32, the same
+// numerics as a scalar fmaf loop).  Block tile BM x BN x 32 staged through LDS
+// (k-major, +1 padding: the transposing stores are conflict-free), 4 waves in
+// 2 x 2, each (BM/2) x (BN/2) as 32 x 32 MFMA tiles; the next k-tile's global
+// loads are in flight in registers while the current one is multiplied.
+// Epilogues fused into the store:
+//   kEpiNone   C = acc
+//   kEpiBias   z = acc + bias[n]; C = z; H = swish(z) if H (flax.linen.swish)
+//   kEpiDSwish C = acc * swish'(Z[m, n])  (gradient through the activation)
+// WG (weight gradients, split-K over the batch): block z multiplies rows
+// [z*KC, (z+1)*KC) into part[z][M+1][N]; row M is the bias gradient, the
+// column sums of the B tile (op(B) = layer-output gradient), which blocks with
+// blockIdx.y == 0 form on the VALU beside the MFMAs.
+constexpr int MBK = 32;
+enum { kEpiNone = 0, kEpiBias = 1, kEpiDSwish = 2 };
 
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
-                                                   const float* __restrict__ B, int ldb, float* __restrict__ C,
-                                                   int ldc, int accumulate) {
-  __shared__ float As[GK][GT + 1];
-  __shared__ float Bs[GK][GT + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += GK) {
-    for (int e = threadIdx.x; e < GT * GK; e += 256) {
-      const int mm = TA ? (e % GT) : (e / GK), kk = TA ? (e / GT) : (e % GK);
+__device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+template <int BM, int BN, bool TA, bool TB, bool WG>
+__global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                    const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                    int ldc, int epi, const float* __restrict__ bias,
+                                                    float* __restrict__ H, const float* __restrict__ Z, int KC) {
+  constexpr int NA = BM * MBK / 256, NB = BN * MBK / 256;  // tile elements per thread
+  constexpr int TM = BM / 64, TN = BN / 64;                // 32x32 tiles per wave
+  __shared__ float As[MBK][BM + 1];
+  __shared__ float Bs[MBK][BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = WG ? blockIdx.z * KC : 0;
+  const int kend = WG ? min(K, kbeg + KC) : K;
+  float ra[NA], rb[NB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + 256 * i;
+      const int mm = TA ? (e % BM) : (e / MBK), kk = TA ? (e / BM) : (e % MBK);
       const int m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < M && k < K) ? (TA ? A[(long long)k * lda + m] : A[(long long)m * lda + k]) : 0.f;
-      const int nn = TB ? (e / GK) : (e % GT), kb = TB ? (e % GK) : (e / GT);
-      const int n = n0 + nn, kq = k0 + kb;
-      Bs[kb][nn] = (n < N && kq < K) ? (TB ? B[(long long)n * ldb + kq] : B[(long long)kq * ldb + n]) : 0.f;
+      ra[i] = (m < M && k < kend) ? (TA ? A[(long long)k * lda + m] : A[(long long)m * lda + k]) : 0.f;
     }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = tid + 256 * i;
+      const int nn = TB ? (e / MBK) : (e % BN), kk = TB ? (e % MBK) : (e / BN);
+      const int n = n0 + nn, k = k0 + kk;
+      rb[i] = (n < N && k < kend) ? (TB ? B[(long long)n * ldb + k] : B[(long long)k * ldb + n]) : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + 256 * i;
+      As[TA ? (e / BM) : (e % MBK)][TA ? (e % BM) : (e / MBK)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = tid + 256 * i;
+      Bs[TB ? (e % MBK) : (e / BN)][TB ? (e / MBK) : (e % BN)] = rb[i];
+    }
+  };
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx16{0};
+  // bias-gradient column sums (WG, blockIdx.y == 0): column cc, k-quarter cq
+  constexpr int CQ = 256 / BN, CK = MBK / CQ;
+  const int cc = tid % BN, cq = tid / BN;
+  float csum = 0.f;
+  const bool do_cs = WG && blockIdx.y == 0;
+  const int r = lane & 31, h = lane >> 5;
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += MBK) {
+    store();
     __syncthreads();
+    if (k0 + MBK < kend) load(k0 + MBK);
 #pragma unroll
-    for (int kk = 0; kk < GK; ++kk) {
-      float a[4], b[4];
+    for (int kb = 0; kb < MBK; kb += 2) {
+      float a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+      for (int i = 0; i < TM; ++i) a[i] = As[kb + h][wm0 + 32 * i + r];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+      for (int j = 0; j < TN; ++j) b[j] = Bs[kb + h][wn0 + 32 * j + r];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (do_cs) {
+#pragma unroll
+      for (int kk = 0; kk < CK; ++kk) csum += Bs[cq * CK + kk][cc];
     }
     __syncthreads();
   }
+  if (WG) {
+    float* P = C + (long long)blockIdx.z * (M + 1) * N;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + ty * 4 + i, n = n0 + tx * 4 + j;
-      if (m < M && n < N) {
-        float* c = C + (long long)m * ldc + n;
-        *c = accumulate ? *c + acc[i][j] : acc[i][j];
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
+          if (m < M && n < N) P[(long long)m * N + n] = acc[i][j][q];
+        }
+    if (do_cs) {
+      float* red = &As[0][0];  // free after the loop's last barrier
+      red[cq * BN + cc] = csum;
+      __syncthreads();
+      if (cq == 0 && n0 + cc < N) {
+        float v = red[cc];
+        for (int q = 1; q < CQ; ++q) v = v + red[q * BN + cc];
+        P[(long long)M * N + n0 + cc] = v;
       }
     }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
+        if (m < M && n < N) {
+          const long long o = (long long)m * ldc + n;
+          float v = acc[i][j][q];
+          if (epi == kEpiBias) {
+            v = v + bias[n];
+            if (H) H[o] = v * sigmoidf(v);
+          } else if (epi == kEpiDSwish) {
+            const float z = Z[o], sg = sigmoidf(z);
+            v = v * (sg + z * sg * (1.0f - sg));
+          }
+          C[o] = v;
+        }
+      }
 }
 
-int gemm(bool ta, bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
-         int ldc, bool accumulate, hipStream_t st) {
+template <int T>
+void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                 hipStream_t st, int epi, const float* bias, float* H, const float* Z) {
+  const dim3 grid((N + T - 1) / T, (M + T - 1) / T);
+  if (!tb)
+    hipLaunchKernelGGL((mgemm_kernel<T, T, false, false, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, epi, bias, H, Z, 0);
+  else
+    hipLaunchKernelGGL((mgemm_kernel<T, T, false, true, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
+                       ldc, epi, bias, H, Z, 0);
+}
+
+// C = A . op(B) with A row-major [M][K]; 128 x 128 tiles when they give at
+// least 512 blocks, 64 x 64 otherwise.
+int gemm(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+         hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
+         const float* Z = nullptr) {
   if (M <= 0 || N <= 0) return ZF_OK;
-  const dim3 grid((N + GT - 1) / GT, (M + GT - 1) / GT);
-  const int acc = accumulate ? 1 : 0;
-  if (!ta && !tb) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
-  else hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, acc);
-  ZF_CHECK_LAUNCH("gemm_kernel");
+  const long long big = (long long)((N + 127) / 128) * ((M + 127) / 128);
+  if (big >= 512) gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z);
+  else gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z);
+  ZF_CHECK_LAUNCH("mgemm_kernel");
   return ZF_OK;
 }
 
 inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
-// ---- per-column reductions (deterministic: one thread per column) ---------
-// out[n] (+)= sum_b X[b, n] * (Y ? Y[b, n] : 1)
-__global__ void colsum_kernel(const float* __restrict__ X, const float* __restrict__ Y, int B, int N,
-                              float* __restrict__ out, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+// Split-K workspace (floats) shared by the batch reductions below.
+constexpr int64_t kWsFloats = 8ll << 20;
+
+// Block: 32 consecutive elements x 8 split lanes; lane l sums splits
+// l, l+8, ... and the lanes combine in a fixed order.
+__global__ __launch_bounds__(256) void wgrad_final(int M, int N, int nsplit, const float* __restrict__ part,
+                                                   float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float red[8][33];
+  const int e = threadIdx.x & 31, l = threadIdx.x >> 5;
+  const long long idx = (long long)blockIdx.x * 32 + e;
+  const long long MN1 = (long long)(M + 1) * N;
+  float s = 0.f;
+  if (idx < MN1)
+    for (int k = l; k < nsplit; k += 8) s += part[k * MN1 + idx];
+  red[l][e] = s;
+  __syncthreads();
+  if (l == 0 && idx < MN1) {
+    const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
+                    ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e]));
+    if (idx < (long long)M * N) dW[idx] = v;
+    else db[idx - (long long)M * N] = v;
+  }
+}
+
+// dW[M,N] = A^T . G and db[N] = colsum(G), A row-major [B][M] (layer input),
+// G row-major [B][N] (gradient of the layer output); the split partials are
+// summed in a fixed order by wgrad_final, so the result is deterministic.
+int wgrad(int M, int N, int B, const float* A, const float* G, float* dW, float* db, float* ws, hipStream_t st) {
+  constexpr int T = 64;
+  // ~2048 blocks in flight, partials within the workspace
+  const int tiles = ((N + T - 1) / T) * ((M + T - 1) / T);
+  int nsplit = (int)std::min<int64_t>(std::min<int64_t>((B + MBK - 1) / MBK, std::max(1, 2048 / tiles)),
+                                      kWsFloats / ((int64_t)(M + 1) * N));
+  nsplit = nsplit < 1 ? 1 : nsplit;
+  int KC = (B + nsplit - 1) / nsplit;
+  KC = (KC + MBK - 1) / MBK * MBK;
+  nsplit = (B + KC - 1) / KC;
+  hipLaunchKernelGGL((mgemm_kernel<T, T, true, false, true>), dim3((N + T - 1) / T, (M + T - 1) / T, nsplit),
+                     dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, KC);
+  ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
+  hipLaunchKernelGGL(wgrad_final, dim3(blocks_for((int64_t)(M + 1) * N, 32)), dim3(256), 0, st, M, N, nsplit, ws, dW, db);
+  ZF_CHECK_LAUNCH("wgrad_final");
+  return ZF_OK;
+}
+
+// ---- per-column sums (split over row chunks, fixed-order final sum) ---------
+// out[n] = sum_b X[b, n] * (Y ? Y[b, n] : 1), N <= 64 columns.
+constexpr int kColChunk = 256;
+
+__global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ X, const float* __restrict__ Y, int B,
+                                                      int N, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int n = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int b0 = blockIdx.x * kColChunk, b1 = min(B, b0 + kColChunk);
+  float s = 0.f;
+  if (n < N)
+    for (int b = b0 + rg; b < b1; b += 4) {
+      const float x = X[(long long)b * N + n];
+      s += Y ? x * Y[(long long)b * N + n] : x;
+    }
+  red[rg][n] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) part[(long long)blockIdx.x * N + n] = (red[0][n] + red[1][n]) + (red[2][n] + red[3][n]);
+}
+
+__global__ void colsum_final(const float* __restrict__ part, int nblk, int N, float* __restrict__ out) {
+  const int n = threadIdx.x;
   if (n >= N) return;
   double s = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const float x = X[(long long)b * N + n];
-    s += Y ? (double)x * (double)Y[(long long)b * N + n] : (double)x;
-  }
-  out[n] = accumulate ? out[n] + (float)s : (float)s;
+  for (int k = 0; k < nblk; ++k) s += (double)part[(long long)k * N + n];
+  out[n] = (float)s;
+}
+
+int colsum(const float* X, const float* Y, int B, int N, float* out, float* ws, hipStream_t st) {
+  const int nblk = (B + kColChunk - 1) / kColChunk;
+  hipLaunchKernelGGL(colsum_partial, dim3(nblk), dim3(256), 0, st, X, Y, B, N, ws);
+  ZF_CHECK_LAUNCH("colsum_partial");
+  hipLaunchKernelGGL(colsum_final, dim3(1), dim3(64), 0, st, ws, nblk, N, out);
+  ZF_CHECK_LAUNCH("colsum_final");
+  return ZF_OK;
 }
 
 // ---- ShiftBounds (train mode; bijectors.py:163-273) -------------------------
@@ -202,28 +379,6 @@ __global__ void bn_apply_kernel(const float* __restrict__ U, const float* __rest
   Ubn[i] = uh * scale[k] + bias[k];
 }
 
-__device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
-
-// Z += bias; H = swish(Z) (flax.linen.swish = z * sigmoid(z)).  act = 0: H = Z.
-__global__ void bias_act_kernel(float* __restrict__ Z, const float* __restrict__ bias, float* __restrict__ H,
-                                int B, int N, int act) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)B * N) return;
-  const float z = Z[i] + bias[i % N];
-  Z[i] = z;
-  if (act) H[i] = z * sigmoidf(z);
-}
-
-// gZ = gH * swish'(Z), swish'(z) = s + z s (1 - s)
-__global__ void swish_bwd_kernel(const float* __restrict__ gH, const float* __restrict__ Z, float* __restrict__ gZ,
-                                 long long n) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float z = Z[i];
-  const float s = sigmoidf(z);
-  gZ[i] = gH[i] * (s + z * s * (1.0f - s));
-}
-
 __device__ __forceinline__ float sp_f(float x) { return 0.5f * (x + sqrtf(x * x + 4.0f)); }
 __device__ __forceinline__ float sp_grad(float x) { return 0.5f * (1.0f + x / sqrtf(x * x + 4.0f)); }
 
@@ -232,36 +387,41 @@ constexpr int kMaxK = 64;
 // One (row, transformed dim): normalize_spline_params (utils.py:37-62) of the
 // raw conditioner outputs p[0..3K-1), bin, RQ spline forward (utils.py:65-141).
 // With grads: reverse pass for gy (dL/dy) and gl (dL/dlog_det): dL/dx and dL/dp.
+// No per-thread arrays (they would live in scratch): the normalised widths and
+// heights are recomputed from p where needed, in the same float order.
+// gp may alias p (in-place reverse): every p[j] is read before gp[j] is written.
 template <bool GRAD>
-__device__ void spline_row(const float* __restrict__ p, int K, float x, float& y, float& ld, float gy, float gl,
-                           float* gx, float* __restrict__ gp) {
+__device__ __forceinline__ void spline_one(const float* p, int K, float x, float& y, float& ld, float gy, float gl,
+                                           float* gx, float* gp) {
   const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // utils.py:32-34, Python floats
   const float cc = (float)c64, norm = (float)(1.0 + c64 * (double)K);
-  float w[kMaxK], h[kMaxK], sa[kMaxK], sb[kMaxK];
   float Sa = 0.f, Sb = 0.f;
   for (int j = 0; j < K; ++j) {
-    sa[j] = sp_f(p[j]);
-    sb[j] = sp_f(p[K + j]);
-    Sa = Sa + sa[j];
-    Sb = Sb + sb[j];
+    Sa = Sa + sp_f(p[j]);
+    Sb = Sb + sp_f(p[K + j]);
   }
-  for (int j = 0; j < K; ++j) {
-    w[j] = (sa[j] / Sa + cc) / norm;
-    h[j] = (sb[j] / Sb + cc) / norm;
-  }
-  // bin: count semantics of _index (utils.py:244-250)
+  // bin: count semantics of _index (utils.py:244-250); the knots t_j are
+  // non-decreasing, so the last knot <= x is knot cnt - 1 and its prefix sums
+  // are the bin's left edge (xk, yk)
   float xk = 0.f, yk = 0.f;
   int cnt = 0;
   {
-    float t = 0.f;
+    float tx = 0.f, ty = 0.f;
     for (int j = 0; j <= K; ++j) {
-      if (t <= x) ++cnt;
-      if (j < K) t = t + w[j];
+      if (tx <= x) {
+        ++cnt;
+        xk = tx;
+        yk = ty;
+      }
+      if (j < K) {
+        tx = tx + (sp_f(p[j]) / Sa + cc) / norm;
+        ty = ty + (sp_f(p[K + j]) / Sb + cc) / norm;
+      }
     }
   }
   int idx = cnt - 1;
   idx = idx < 0 ? 0 : (idx > K ? K : idx);
-  for (int j = 0; j < idx; ++j) { xk = xk + w[j]; yk = yk + h[j]; }
+  if (cnt == 0) xk = yk = 0.f;
   const bool oob = (x < 0.f) || (x >= 1.f);
   if (idx == K || oob) {
     // idx == K: the reference's fill-mode gather gives NaN (utils.py:224-230);
@@ -274,7 +434,7 @@ __device__ void spline_row(const float* __restrict__ p, int K, float x, float& y
     }
     return;
   }
-  const float wk = w[idx], hk = h[idx];
+  const float wk = (sp_f(p[idx]) / Sa + cc) / norm, hk = (sp_f(p[K + idx]) / Sb + cc) / norm;
   const float dk = (idx == 0) ? 1.f : sp_f(p[2 * K + idx - 1]);
   const float dk1 = (idx + 1 == K) ? 1.f : sp_f(p[2 * K + idx]);
   const float sk = hk / wk;
@@ -312,65 +472,103 @@ __device__ void spline_row(const float* __restrict__ p, int K, float x, float& y
   float g_wk = -g_zr * zr / wk;
   g_hk += g_sk / wk;
   g_wk += -g_sk * hk / (wk * wk);
-  // scatter to widths / heights: xk = sum_{j<idx} w_j, yk likewise
-  float gw[kMaxK], gh[kMaxK];
-  for (int j = 0; j < K; ++j) {
-    gw[j] = (j < idx) ? g_xk : 0.f;
-    gh[j] = (j < idx) ? g_yk : 0.f;
-  }
-  gw[idx] += g_wk;
-  gh[idx] += g_hk;
-  // normalisation: w_j = (sa_j / Sa + c) / norm
+  // gradient w.r.t. widths / heights: xk = sum_{j<idx} w_j (likewise yk), plus
+  // the bin's own w_idx, h_idx; then through w_j = (sa_j / Sa + c) / norm
+  auto gw = [&](int j) { return j < idx ? g_xk : (j == idx ? g_wk : 0.f); };
+  auto gh = [&](int j) { return j < idx ? g_yk : (j == idx ? g_hk : 0.f); };
   float tw = 0.f, th = 0.f;
-  for (int j = 0; j < K; ++j) { tw += gw[j] * sa[j]; th += gh[j] * sb[j]; }
   for (int j = 0; j < K; ++j) {
-    const float gsa = (gw[j] / Sa - tw / (Sa * Sa)) / norm;
-    const float gsb = (gh[j] / Sb - th / (Sb * Sb)) / norm;
+    tw += gw(j) * sp_f(p[j]);
+    th += gh(j) * sp_f(p[K + j]);
+  }
+  const float gd0 = idx >= 1 ? g_dk * sp_grad(p[2 * K + idx - 1]) : 0.f;
+  const float gd1 = idx + 1 < K ? g_dk1 * sp_grad(p[2 * K + idx]) : 0.f;
+  for (int j = 0; j < K; ++j) {
+    const float gsa = (gw(j) / Sa - tw / (Sa * Sa)) / norm;
+    const float gsb = (gh(j) / Sb - th / (Sb * Sb)) / norm;
     gp[j] = gsa * sp_grad(p[j]);
     gp[K + j] = gsb * sp_grad(p[K + j]);
   }
   for (int j = 0; j < K - 1; ++j) gp[2 * K + j] = 0.f;
-  if (idx >= 1) gp[2 * K + idx - 1] += g_dk * sp_grad(p[2 * K + idx - 1]);
-  if (idx + 1 < K) gp[2 * K + idx] += g_dk1 * sp_grad(p[2 * K + idx]);
+  if (idx >= 1) gp[2 * K + idx - 1] = 0.f + gd0;
+  if (idx + 1 < K) gp[2 * K + idx] = 0.f + gd1;
 }
 
-// Forward: transformed dims (logical d < dt at column pmod(d + rot, D)) through
-// the spline; conditioning columns copied; log-det summed in dim order.
-__global__ void spline_fwd_kernel(const float* __restrict__ s_in, float* __restrict__ s_out,
-                                  const float* __restrict__ P, float* __restrict__ ld, int B, int D, int dt, int K,
-                                  int rot) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int S = 3 * K - 1;
-  for (int j = 0; j < D; ++j) s_out[(long long)b * D + j] = s_in[(long long)b * D + j];
-  float l = 0.f;
-  for (int d = 0; d < dt; ++d) {
+// Thread per (row, transformed dim): one-wave blocks of rpb = 64 / dt rows.
+// The block's conditioner outputs P[b0 .. b0+rpb)[dt][S] are contiguous: they
+// are staged through LDS with coalesced loads (thread-major [64][S], S odd for
+// even K so the per-thread rows spread over the banks).  Logical dim d < dt is
+// column pmod(d + rot, D); thread d also carries the conditioning columns
+// dt + d, dt + d + dt, ... through unchanged.
+constexpr int kSplThreads = 64;
+
+__device__ __forceinline__ void stage_rows(float* sp, const float* __restrict__ src, long long n) {
+  for (long long e = threadIdx.x; e < n; e += kSplThreads) sp[e] = src[e];
+}
+
+// Forward: log-det summed per row in dim order through LDS.
+__global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __restrict__ s_in,
+                                                                 float* __restrict__ s_out,
+                                                                 const float* __restrict__ P, float* __restrict__ ld,
+                                                                 int B, int D, int dt, int K, int rot) {
+  extern __shared__ float sp[];
+  __shared__ float lds[kSplThreads];
+  const int S = 3 * K - 1, rpb = kSplThreads / dt;
+  const int lr = threadIdx.x / dt, d = threadIdx.x - lr * dt;
+  const long long b0 = (long long)blockIdx.x * rpb, b = b0 + lr;
+  const int nrows = (int)(B - b0 < rpb ? B - b0 : rpb);
+  stage_rows(sp, P + b0 * dt * S, (long long)nrows * dt * S);
+  __syncthreads();
+  const bool ok = lr < nrows;
+  if (ok) {
+    for (int j = dt + d; j < D; j += dt) {
+      const int cj = pmodi(j + rot, D);
+      s_out[b * D + cj] = s_in[b * D + cj];
+    }
     const int col = pmodi(d + rot, D);
     float y, ldv;
-    spline_row<false>(P + ((long long)b * dt + d) * S, K, s_in[(long long)b * D + col], y, ldv, 0.f, 0.f, nullptr,
-                      nullptr);
-    s_out[(long long)b * D + col] = y;
-    l = l + ldv;
+    spline_one<false>(sp + threadIdx.x * S, K, s_in[b * D + col], y, ldv, 0.f, 0.f, nullptr, nullptr);
+    s_out[b * D + col] = y;
+    lds[threadIdx.x] = ldv;
   }
-  ld[b] = ld[b] + l;
+  __syncthreads();
+  if (ok && d == 0) {
+    float l = 0.f;
+    for (int k = 0; k < dt; ++k) l = l + lds[threadIdx.x + k];
+    ld[b] = ld[b] + l;
+  }
 }
 
 // Reverse: g_in = dL/d(state_in) from g_out = dL/d(state_out) and gl per row;
 // conditioning columns pass g_out through (their MLP share is added later).
-__global__ void spline_bwd_kernel(const float* __restrict__ s_in, const float* __restrict__ P,
-                                  const float* __restrict__ g_out, float gl, float* __restrict__ g_in,
-                                  float* __restrict__ gP, int B, int D, int dt, int K, int rot) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int S = 3 * K - 1;
-  for (int j = 0; j < D; ++j) g_in[(long long)b * D + j] = g_out[(long long)b * D + j];
-  for (int d = 0; d < dt; ++d) {
+// dL/dP is formed in place in the staged rows and written back coalesced.
+__global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __restrict__ s_in,
+                                                                 const float* __restrict__ P,
+                                                                 const float* __restrict__ g_out, float gl,
+                                                                 float* __restrict__ g_in, float* __restrict__ gP,
+                                                                 int B, int D, int dt, int K, int rot) {
+  extern __shared__ float sp[];
+  const int S = 3 * K - 1, rpb = kSplThreads / dt;
+  const int lr = threadIdx.x / dt, d = threadIdx.x - lr * dt;
+  const long long b0 = (long long)blockIdx.x * rpb, b = b0 + lr;
+  const int nrows = (int)(B - b0 < rpb ? B - b0 : rpb);
+  const long long n = (long long)nrows * dt * S;
+  stage_rows(sp, P + b0 * dt * S, n);
+  __syncthreads();
+  if (lr < nrows) {
+    for (int j = dt + d; j < D; j += dt) {
+      const int cj = pmodi(j + rot, D);
+      g_in[b * D + cj] = g_out[b * D + cj];
+    }
     const int col = pmodi(d + rot, D);
     float y, ldv, gx;
-    spline_row<true>(P + ((long long)b * dt + d) * S, K, s_in[(long long)b * D + col], y, ldv,
-                     g_out[(long long)b * D + col], gl, &gx, gP + ((long long)b * dt + d) * S);
-    g_in[(long long)b * D + col] = gx;
+    float* row = sp + threadIdx.x * S;
+    spline_one<true>(row, K, s_in[b * D + col], y, ldv, g_out[b * D + col], gl, &gx, row);
+    g_in[b * D + col] = gx;
   }
+  __syncthreads();
+  float* dst = gP + b0 * dt * S;
+  for (long long e = threadIdx.x; e < n; e += kSplThreads) dst[e] = sp[e];
 }
 
 // BatchNorm reverse with batch statistics:
@@ -510,6 +708,7 @@ struct zf_trainer {
   double* d_dsmall = nullptr;
   double* d_part = nullptr;
   void* d_colws = nullptr;
+  float* d_ws = nullptr;      // split-K partials (kWsFloats)
   int64_t colws_bytes = 0;
   struct NscBufs {
     float *U, *Uhat, *Ubn, *P, *gP, *gU, *gA, *gB;
@@ -557,7 +756,7 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   int rc = zf_flow_plan(&desc, &need);
   if (rc) return rc;
   if (need != blob_floats) return zf::einval("blob has %lld floats, plan needs %lld", (long long)blob_floats, (long long)need);
-  if (batch_max < 1) return zf::einval("batch_max < 1");
+  if (batch_max < 1 || batch_max > (1 << 24)) return zf::einval("batch_max outside [1, 2^24]");
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind == ZF_OP_SHIFT_BOUNDS && i != 0)
@@ -596,6 +795,7 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_small = zf::dmalloc(t, 8 * 256, rc);
   t->d_dsmall = (double*)zf::dmalloc(t, 4 * 256, rc);
   t->d_part = (double*)zf::dmalloc(t, 2 * ((B + 255) / 256 + 1), rc);
+  t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
   t->colws_bytes = zf_colstats_workspace_bytes(B, 64);
   t->d_colws = zf::dmalloc(t, t->colws_bytes / 4 + 1, rc);
   t->nsc.resize(desc.n_ops);
@@ -703,17 +903,17 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
         const bool last = (l == op.n_hidden);
         const int out_w = last ? dt * S : op.hidden[l];
         float* Z = last ? nb.P : nb.Z[l];
-        rc = zf::gemm(false, false, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, false, st);
+        rc = zf::gemm(false, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
+                      nat + op.off_b[l], last ? nullptr : nb.H[l]);
         if (rc) return rc;
-        hipLaunchKernelGGL(zf::bias_act_kernel, dim3(zf::blocks_for((int64_t)B * out_w)), dim3(256), 0, st, Z,
-                           nat + op.off_b[l], last ? nullptr : nb.H[l], B, out_w, last ? 0 : 1);
-        ZF_CHECK_LAUNCH("bias_act_kernel");
         if (!last) {
           in = nb.H[l];
           in_w = out_w;
         }
       }
-      hipLaunchKernelGGL(zf::spline_fwd_kernel, dim3(zf::blocks_for(B, 64)), dim3(64), 0, st, sin, sout, nb.P,
+      const int rpb = zf::kSplThreads / dt;
+      hipLaunchKernelGGL(zf::spline_fwd_kernel, dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),
+                         (size_t)zf::kSplThreads * S * sizeof(float), st, sin, sout, nb.P,
                          t->d_ld, B, D, dt, op.knots, rot);
       ZF_CHECK_LAUNCH("spline_fwd_kernel");
     } else {
@@ -749,7 +949,9 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
     zf_trainer::NscBufs& nb = t->nsc[i];
     const int r = rots[i];
     // spline: g -> g_prev (transformed columns), gP
-    hipLaunchKernelGGL(zf::spline_bwd_kernel, dim3(zf::blocks_for(B, 64)), dim3(64), 0, st, state(i), nb.P, g, gl,
+    const int rpb = zf::kSplThreads / dt;
+    hipLaunchKernelGGL(zf::spline_bwd_kernel, dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),
+                       (size_t)zf::kSplThreads * S * sizeof(float), st, state(i), nb.P, g, gl,
                        g_prev, nb.gP, B, D, dt, op.knots, r);
     ZF_CHECK_LAUNCH("spline_bwd_kernel");
     // MLP reverse
@@ -761,19 +963,15 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
       const int in_w = l == 0 ? DC : op.hidden[l - 1];
       const float* hin = l == 0 ? nb.Ubn : nb.H[l - 1];
       // dW_l = hin^T . gout ; db_l = colsum(gout)
-      rc = zf::gemm(true, false, in_w, out_w, B, hin, in_w, gout, out_w, G + op.off_w[l], out_w, false, st);
+      rc = zf::wgrad(in_w, out_w, B, hin, gout, G + op.off_w[l], G + op.off_b[l], t->d_ws, st);
       if (rc) return rc;
-      hipLaunchKernelGGL(zf::colsum_kernel, dim3(zf::blocks_for(out_w, 128)), dim3(128), 0, st, gout, nullptr, B,
-                         out_w, G + op.off_b[l], 0);
-      ZF_CHECK_LAUNCH("colsum_kernel");
       // g_in = gout . W_l^T
       float* gin = l == 0 ? nb.gU : gbufs[which];
-      rc = zf::gemm(false, true, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, false, st);
+      // (through swish of layer l-1 when l > 0)
+      rc = zf::gemm(true, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
+                    l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr);
       if (rc) return rc;
-      if (l > 0) {  // through swish of layer l-1
-        hipLaunchKernelGGL(zf::swish_bwd_kernel, dim3(zf::blocks_for((int64_t)B * in_w)), dim3(256), 0, st, gin,
-                           nb.Z[l - 1], gin, (long long)B * in_w);
-        ZF_CHECK_LAUNCH("swish_bwd_kernel");
+      if (l > 0) {
         gout = gin;
         out_w = in_w;
         which ^= 1;
@@ -782,10 +980,10 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
     // BatchNorm: gU holds d loss / d Ubn
     float* bn = nat + op.off_bn;
     float* gbn = G + op.off_bn;
-    hipLaunchKernelGGL(zf::colsum_kernel, dim3(1), dim3(128), 0, st, nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, 0);
-    ZF_CHECK_LAUNCH("colsum_kernel");
-    hipLaunchKernelGGL(zf::colsum_kernel, dim3(1), dim3(128), 0, st, nb.gU, nullptr, B, DC, gbn + 3 * DC, 0);
-    ZF_CHECK_LAUNCH("colsum_kernel");
+    rc = zf::colsum(nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, t->d_ws, st);
+    if (rc) return rc;
+    rc = zf::colsum(nb.gU, nullptr, B, DC, gbn + 3 * DC, t->d_ws, st);
+    if (rc) return rc;
     // gU := d loss / d U, in place (reads each element before writing it)
     hipLaunchKernelGGL(zf::bn_bwd_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.gU, nb.Uhat,
                        bn + 2 * DC, nb.rstd, gbn + 3 * DC, gbn + 2 * DC, nb.gU, B, DC);

@@ -112,9 +112,12 @@ class Trainer:
 
     def step(self, x, c=None) -> None:
         xd, cd = self._dev(x, self.D), self._dev(c, self.C)
-        check(L.load_library().zf_trainer_step(
-            self.handle, xd.ptr, None if cd is None else cd.ptr, xd.shape[0], self._loss.ptr, L.stream()),
-            "zf_trainer_step")
+        self._step_rows(xd.ptr, None if cd is None else cd.ptr, xd.shape[0])
+
+    def _step_rows(self, xptr: int, cptr: Optional[int], rows: int) -> None:
+        """One step on ``rows`` device-resident rows (raw pointers; async)."""
+        check(L.load_library().zf_trainer_step(self.handle, xptr, cptr, rows, self._loss.ptr, L.stream()),
+              "zf_trainer_step")
 
     def last_loss(self) -> float:
         return float(self._loss.numpy()[0])
@@ -186,21 +189,25 @@ def train(
         except ModuleNotFoundError:  # pragma: no cover
             pass
 
-    X_dev = DeviceArray.from_numpy(X_train)
-    C_dev = None if C_train is None else DeviceArray.from_numpy(C_train)
     loss_train: List[float] = []
     loss_test: List[float] = []
     best_epoch = 0
     best_variables = variables
     X = C = None
+    n = X_train.shape[0]
     for epoch in loop:
-        perm = np.random.default_rng([seed, epoch]).permutation(X_train.shape[0])
+        perm = np.random.default_rng([seed, epoch]).permutation(n)
         X_perm = X_train[perm]
         C_perm = None if C_train is None else C_train[perm]
-        for batch_idx in range(0, len(X_perm), batch_size):
-            X = X_perm[batch_idx : batch_idx + batch_size]
-            C = None if C_perm is None else C_perm[batch_idx : batch_idx + batch_size]
-            trainer.step(X, C)
+        # one upload per epoch; batches are row ranges of the resident copy
+        X_dev = DeviceArray.from_numpy(X_perm)
+        C_dev = None if C_perm is None else DeviceArray.from_numpy(C_perm)
+        for batch_idx in range(0, n, batch_size):
+            rows = min(batch_size, n - batch_idx)
+            trainer._step_rows(X_dev.ptr + batch_idx * D * 4,
+                               None if C_dev is None else C_dev.ptr + batch_idx * Cd * 4, rows)
+        X = X_perm[batch_idx : batch_idx + batch_size]
+        C = None if C_perm is None else C_perm[batch_idx : batch_idx + batch_size]
 
         variables = trainer.variables()
         loss_train.append(_metric(flow, variables, X, C))  # last batch, as train.py:122
@@ -217,5 +224,4 @@ def train(
         if epoch >= warmup and epoch >= 2 * patience and epoch % patience == 0:
             if not np.min(loss_test[-patience:]) < np.min(loss_test[-2 * patience : -patience]):
                 break
-    del X_dev, C_dev
     return best_variables, best_epoch, loss_train, loss_test
