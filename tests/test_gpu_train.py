@@ -158,3 +158,28 @@ def test_train_end_to_end_two_moons():
     lp = flow.apply(best, X[3000:])
     assert np.isfinite(lp).mean() > 0.99
     assert -lp.mean() == pytest.approx(ls[best_epoch], rel=1e-5)
+
+
+def test_step_graph_matches_eager(monkeypatch):
+    """zf_trainer_step replays one captured hipGraph per batch size; the
+    graph and the eagerly launched step give bit-identical parameters (every
+    reduction has a fixed order), including a ragged last batch."""
+    from zenflow_amd.io import flatten_variables
+    from zenflow_amd.train import Trainer
+
+    flat = []
+    losses = []
+    for graph in ("1", "0"):
+        monkeypatch.setenv("ZF_TRAIN_GRAPH", graph)
+        case, flow, _ = _setup("cfg4", 300, 65)
+        tr = Trainer(flow, case["variables"], 2, 2, 256)
+        x, c = case["x"], case["c"]
+        for _ in range(3):
+            tr.step(x[:256], c[:256])
+            tr.step(x[256:], c[256:])
+        losses.append(tr.last_loss())
+        flat.append(flatten_variables(tr.variables()))
+    assert losses[0] == losses[1]
+    assert flat[0].keys() == flat[1].keys()
+    for k in flat[0]:
+        np.testing.assert_array_equal(flat[0][k], flat[1][k], err_msg=k)

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
+#include <map>
 #include <vector>
 
 namespace zf {
@@ -502,8 +504,31 @@ __device__ __forceinline__ void spline_one(const float* p, int K, float x, float
 // dt + d, dt + d + dt, ... through unchanged.
 constexpr int kSplThreads = 64;
 
+// Global <-> LDS copies of n floats, 8 loads in flight per lane.
 __device__ __forceinline__ void stage_rows(float* sp, const float* __restrict__ src, long long n) {
-  for (long long e = threadIdx.x; e < n; e += kSplThreads) sp[e] = src[e];
+  for (long long e0 = threadIdx.x; e0 < n; e0 += 8 * kSplThreads) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long e = e0 + u * kSplThreads;
+      v[u] = e < n ? src[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long e = e0 + u * kSplThreads;
+      if (e < n) sp[e] = v[u];
+    }
+  }
+}
+
+__device__ __forceinline__ void unstage_rows(float* __restrict__ dst, const float* sp, long long n) {
+  for (long long e0 = threadIdx.x; e0 < n; e0 += 8 * kSplThreads) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long e = e0 + u * kSplThreads;
+      if (e < n) dst[e] = sp[e];
+    }
+  }
 }
 
 // Forward: log-det summed per row in dim order through LDS.
@@ -567,8 +592,7 @@ __global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __
     g_in[b * D + col] = gx;
   }
   __syncthreads();
-  float* dst = gP + b0 * dt * S;
-  for (long long e = threadIdx.x; e < n; e += kSplThreads) dst[e] = sp[e];
+  unstage_rows(gP + b0 * dt * S, sp, n);
 }
 
 // BatchNorm reverse with batch statistics:
@@ -583,6 +607,106 @@ __global__ void bn_bwd_kernel(const float* __restrict__ gUbn, const float* __res
   // sum_g / sum_gu are sums of gUbn and gUbn*Uhat; scale them into gUhat terms
   const float mg = scale[k] * sum_g[k] / B, mgu = scale[k] * sum_gu[k] / B;
   gU[i] = rstd[k] * (gUbn[i] * scale[k] - mg - Uhat[i] * mgu);
+}
+
+// ---- small batches: BatchNorm forward / reverse in one single-block launch --
+// (B * DC <= kBnSmall).  Same arithmetic as gather_u + colstats + bn_stats +
+// bn_apply (forward) and colsum x2 + bn_bwd + scatter (reverse); the column
+// sums are fp64 over a fixed thread layout (column k = tid % DC, row lane
+// tid / DC) combined in lane order, so the result is deterministic.
+constexpr long long kBnSmall = 1ll << 14;
+
+__global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s, const float* __restrict__ c,
+                                                     float* __restrict__ Uhat, float* __restrict__ Ubn,
+                                                     float* __restrict__ nat_bn, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int B, int D, int C, int dt, int dc,
+                                                     int rot, int update) {
+  __shared__ double ssum[1024], ssq[1024];
+  __shared__ float smean[64], srstd[64];
+  const int DC = dc + C, L = 1024 / DC, tid = threadIdx.x;
+  const int k = tid % DC, l = tid / DC;
+  auto u_at = [&](long long b, int kk) { return kk < dc ? s[b * D + pmodi(dt + kk + rot, D)] : c[b * C + (kk - dc)]; };
+  double sm = 0.0, sq = 0.0;
+  if (l < L)
+    for (long long b = l; b < B; b += L) {
+      const double u = (double)u_at(b, k);
+      sm += u;
+      sq += u * u;
+    }
+  ssum[tid] = sm;
+  ssq[tid] = sq;
+  __syncthreads();
+  if (tid < DC) {
+    double a = 0.0, q = 0.0;
+    for (int j = 0; j < L; ++j) {
+      a += ssum[j * DC + tid];
+      q += ssq[j * DC + tid];
+    }
+    const float mean = (float)(a / B), mean2 = (float)(q / B);
+    const float var = fmaxf(0.f, mean2 - mean * mean);
+    const float rstd = 1.0f / sqrtf(var + kBnEps);
+    smean[tid] = mean;
+    srstd[tid] = rstd;
+    mean_out[tid] = mean;
+    rstd_out[tid] = rstd;
+    if (update) {
+      nat_bn[tid] = kBnMomentum * nat_bn[tid] + (1.0f - kBnMomentum) * mean;
+      nat_bn[DC + tid] = kBnMomentum * nat_bn[DC + tid] + (1.0f - kBnMomentum) * var;
+    }
+  }
+  __syncthreads();
+  const float* scale = nat_bn + 2 * DC;
+  const float* bias = nat_bn + 3 * DC;
+  for (long long i = tid; i < (long long)B * DC; i += 1024) {
+    const long long b = i / DC;
+    const int kk = (int)(i - b * DC);
+    const float uh = (u_at(b, kk) - smean[kk]) * srstd[kk];
+    Uhat[i] = uh;
+    Ubn[i] = uh * scale[kk] + bias[kk];
+  }
+}
+
+// gUbn = dL/dUbn -> BatchNorm scale / bias gradients and dL/dU; the
+// conditioning columns' share is added to g (dL/d state) in place.
+__global__ __launch_bounds__(1024) void bn_bwd_small(const float* __restrict__ gUbn, const float* __restrict__ Uhat,
+                                                     const float* __restrict__ scale, const float* __restrict__ rstd,
+                                                     float* __restrict__ g_scale, float* __restrict__ g_bias,
+                                                     float* __restrict__ g, int B, int D, int C, int dt, int dc,
+                                                     int rot) {
+  __shared__ double sgu[1024], sg[1024];
+  __shared__ float mg_s[64], mgu_s[64];
+  const int DC = dc + C, L = 1024 / DC, tid = threadIdx.x;
+  const int k = tid % DC, l = tid / DC;
+  double a = 0.0, q = 0.0;
+  if (l < L)
+    for (long long b = l; b < B; b += L) {
+      const float gv = gUbn[b * DC + k];
+      a += (double)(gv * Uhat[b * DC + k]);
+      q += (double)gv;
+    }
+  sgu[tid] = a;
+  sg[tid] = q;
+  __syncthreads();
+  if (tid < DC) {
+    double x = 0.0, y = 0.0;
+    for (int j = 0; j < L; ++j) {
+      x += sgu[j * DC + tid];
+      y += sg[j * DC + tid];
+    }
+    const float sum_gu = (float)x, sum_g = (float)y;
+    g_scale[tid] = sum_gu;
+    g_bias[tid] = sum_g;
+    mg_s[tid] = scale[tid] * sum_g / B;
+    mgu_s[tid] = scale[tid] * sum_gu / B;
+  }
+  __syncthreads();
+  for (long long i = tid; i < (long long)B * dc; i += 1024) {
+    const long long b = i / dc;
+    const int kk = (int)(i - b * dc);
+    const long long e = b * DC + kk;
+    const float gu = rstd[kk] * (gUbn[e] * scale[kk] - mg_s[kk] - Uhat[e] * mgu_s[kk]);
+    g[b * D + pmodi(dt + kk + rot, D)] += gu;
+  }
 }
 
 __global__ void scatter_gu_kernel(const float* __restrict__ gU, float* __restrict__ g, int B, int D, int C, int dt,
@@ -662,12 +786,24 @@ __global__ void sum_partials_kernel(const double* __restrict__ part, int n, doub
 // ---- optimiser: optax adamw / nadamw ---------------------------------------
 // scale_by_adam(b1, b2, eps, nesterov) -> add_decayed_weights(wd) -> scale(-lr)
 // (optax/_src/transform.py, alias.py), masked to the parameter entries.
+// Step count and bias corrections on the device (so a captured step graph
+// replays correctly): bc[0] = step t (as float bits of an int), bc[1] =
+// 1 - b1^t, bc[2] = 1 - b1^(t+1), bc[3] = 1 - b2^t.
+__global__ void step_kernel(float* __restrict__ bc, float b1, float b2) {
+  int* cnt = reinterpret_cast<int*>(bc);
+  const int t = *cnt + 1;
+  *cnt = t;
+  bc[1] = (float)(1.0 - pow((double)b1, (double)t));
+  bc[2] = (float)(1.0 - pow((double)b1, (double)t + 1.0));
+  bc[3] = (float)(1.0 - pow((double)b2, (double)t));
+}
+
 __global__ void adam_kernel(float* __restrict__ prm, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, const unsigned char* __restrict__ mask, long long n, float lr,
-                            float b1, float b2, float eps, float wd, int nesterov, float bc1, float bc1n,
-                            float bc2) {
+                            float b1, float b2, float eps, float wd, int nesterov, const float* __restrict__ bc) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !mask[i]) return;
+  const float bc1 = bc[1], bc1n = bc[2], bc2 = bc[3];
   const float gi = g[i];
   const float mi = b1 * m[i] + (1.0f - b1) * gi;
   const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
@@ -690,7 +826,7 @@ struct zf_trainer {
   int64_t nat_floats = 0;
   int64_t bmax = 0;
   zf_optim_desc opt;
-  long long t = 0;  // optimiser step count
+  long long t = 0;  // optimiser step count (host mirror of d_step)
   std::vector<float> sb_modes, sb_prm;  // ShiftBounds pre-transform per dim (colstats)
   float* d_nat = nullptr;
   float* d_grad = nullptr;
@@ -701,6 +837,13 @@ struct zf_trainer {
   std::vector<float*> bufs;
   std::vector<int64_t> sizes;
   float* d_state = nullptr;   // [n_ops + 1][bmax][D] states before each op
+  float* d_c = nullptr;       // [bmax][C] conditioning inputs of the batch
+  float* d_bc = nullptr;      // optimiser step count + bias corrections (step_kernel)
+  // zf_trainer_step as one hipGraph per batch size (the body reads only the
+  // trainer's own buffers: x and c are copied in before the launch)
+  hipStream_t cap = nullptr;
+  std::map<int64_t, hipGraphExec_t> graphs;
+  bool use_graph = true;
   float* d_ld = nullptr;      // [bmax]
   float* d_g0 = nullptr;      // [bmax][D]
   float* d_g1 = nullptr;
@@ -796,6 +939,16 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_dsmall = (double*)zf::dmalloc(t, 4 * 256, rc);
   t->d_part = (double*)zf::dmalloc(t, 2 * ((B + 255) / 256 + 1), rc);
   t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
+  t->d_c = zf::dmalloc(t, B * (desc.cond_dim > 0 ? desc.cond_dim : 1), rc);
+  t->d_bc = zf::dmalloc(t, 4, rc);
+  {
+    const char* g = std::getenv("ZF_TRAIN_GRAPH");
+    t->use_graph = !(g && g[0] == '0');
+  }
+  if (!rc) {
+    hipError_t e = hipStreamCreateWithFlags(&t->cap, hipStreamNonBlocking);
+    if (e != hipSuccess) rc = zf::hip_status(e, "zf_trainer_create stream");
+  }
   t->colws_bytes = zf_colstats_workspace_bytes(B, 64);
   t->d_colws = zf::dmalloc(t, t->colws_bytes / 4 + 1, rc);
   t->nsc.resize(desc.n_ops);
@@ -827,6 +980,7 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   if (!rc && e == hipSuccess) e = hipMemcpy(t->d_mask, param_mask, need, hipMemcpyHostToDevice);
   if (!rc && e == hipSuccess) e = hipMemset(t->d_m, 0, need * sizeof(float));
   if (!rc && e == hipSuccess) e = hipMemset(t->d_v, 0, need * sizeof(float));
+  if (!rc && e == hipSuccess) e = hipMemset(t->d_bc, 0, 4 * sizeof(float));
   if (!rc && e != hipSuccess) rc = zf::hip_status(e, "zf_trainer_create");
   if (rc) {
     zf_trainer_destroy(t);
@@ -838,23 +992,46 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
 
 int zf_trainer_destroy(zf_trainer_t* t) {
   if (!t) return ZF_OK;
+  (void)hipDeviceSynchronize();
+  for (auto& kv : t->graphs) (void)hipGraphExecDestroy(kv.second);
+  if (t->cap) (void)hipStreamDestroy(t->cap);
   for (float* p : t->bufs) (void)hipFree(p);
   delete t;
   return ZF_OK;
 }
 
-int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_t B64, int update_stats,
-                         double* loss, float* grad, void* stream) {
-  if (!t) return zf::einval("trainer is NULL");
-  if (B64 < 1 || B64 > t->bmax) return zf::einval("batch %lld outside [1, %lld]", (long long)B64, (long long)t->bmax);
-  if (!x) return zf::einval("x is NULL");
-  if (t->C > 0 && !c) return zf::einval("flow is conditional but c is NULL");
-  hipStream_t st = (hipStream_t)stream;
-  const int B = (int)B64, D = t->D, C = t->C;
+}  // extern "C"
+
+namespace zf {
+namespace {
+
+// Copy the batch into the trainer's buffers (state 0, d_c).
+int trainer_stage(zf_trainer_t* t, const float* x, const float* c, int64_t B64, hipStream_t st) {
+  if (!t) return einval("trainer is NULL");
+  if (B64 < 1 || B64 > t->bmax) return einval("batch %lld outside [1, %lld]", (long long)B64, (long long)t->bmax);
+  if (!x) return einval("x is NULL");
+  if (t->C > 0 && !c) return einval("flow is conditional but c is NULL");
+  ZF_TRY_HIP(hipMemcpyAsync(t->d_state, x, (size_t)B64 * t->D * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (t->C > 0)
+    ZF_TRY_HIP(hipMemcpyAsync(t->d_c, c, (size_t)B64 * t->C * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return ZF_OK;
+}
+
+inline double* loss_slot(zf_trainer_t* t, int B) { return t->d_part + blocks_for(B); }
+
+// Train-mode forward + loss + reverse pass from the staged batch; the loss
+// lands in loss_slot(t, B), the gradient in G (natural blob layout).
+int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t st) {
+  const int D = t->D, C = t->C;
+  const float* c = t->d_c;
   const zf_flow_desc& desc = t->desc;
   float* nat = t->d_nat;
-  auto state = [&](int i) { return t->d_state + (int64_t)i * t->bmax * D; };
-  ZF_TRY_HIP(hipMemcpyAsync(state(0), x, (size_t)B * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+  // state before op i; Roll is an index rotation, so it aliases its input
+  std::vector<float*> sp(desc.n_ops + 1);
+  sp[0] = t->d_state;
+  for (int i = 0; i < desc.n_ops; ++i)
+    sp[i + 1] = desc.ops[i].kind == ZF_OP_ROLL ? sp[i] : t->d_state + (int64_t)(i + 1) * t->bmax * D;
+  auto state = [&](int i) { return sp[i]; };
   ZF_TRY_HIP(hipMemsetAsync(t->d_ld, 0, (size_t)B * sizeof(float), st));
   int rc;
   // ---- forward (train mode) ----
@@ -866,13 +1043,12 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
     float* sin = state(i);
     float* sout = state(i + 1);
     if (op.kind == ZF_OP_ROLL) {
-      ZF_TRY_HIP(hipMemcpyAsync(sout, sin, (size_t)B * D * sizeof(float), hipMemcpyDeviceToDevice, st));
       rot = zf::pmodi(rot - op.shift, D);
     } else if (op.kind == ZF_OP_SHIFT_BOUNDS) {
       float* sb = nat + op.off_sb;
       // batch min / max of the (safe_log-transformed) columns (first op: rot == 0)
       rc = zf_colstats(sin, B, D, D, 0, t->sb_modes.data(), t->sb_prm.data(), t->d_small, t->d_small + 64,
-                       nullptr, nullptr, t->d_colws, stream);
+                       nullptr, nullptr, t->d_colws, st);
       if (rc) return rc;
       hipLaunchKernelGGL(zf::sb_stats_kernel, dim3(1), dim3(64), 0, st, sb, D, t->d_small, t->d_small + 64,
                          update_stats);
@@ -884,19 +1060,25 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
       int dt, dc, DC, S;
       zf::nsc_dims(t, op, dt, dc, DC, S);
       zf_trainer::NscBufs& nb = t->nsc[i];
-      hipLaunchKernelGGL(zf::gather_u_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, sin, c, nb.U,
-                         B, D, C, dt, dc, rot);
-      ZF_CHECK_LAUNCH("gather_u_kernel");
-      rc = zf_colstats(nb.U, B, DC, DC, 0, nullptr, nullptr, nullptr, nullptr, t->d_dsmall, t->d_dsmall + 128,
-                       t->d_colws, stream);
-      if (rc) return rc;
       float* bn = nat + op.off_bn;  // [mean, var, scale, bias]
-      hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(128), 0, st, t->d_dsmall, t->d_dsmall + 128, B, DC, bn,
-                         nb.mean, nb.rstd, update_stats);
-      ZF_CHECK_LAUNCH("bn_stats_kernel");
-      hipLaunchKernelGGL(zf::bn_apply_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.U, nb.mean,
-                         nb.rstd, bn + 2 * DC, bn + 3 * DC, nb.Uhat, nb.Ubn, B, DC);
-      ZF_CHECK_LAUNCH("bn_apply_kernel");
+      if ((long long)B * DC <= zf::kBnSmall) {
+        hipLaunchKernelGGL(zf::bn_fwd_small, dim3(1), dim3(1024), 0, st, sin, c, nb.Uhat, nb.Ubn, bn, nb.mean,
+                           nb.rstd, B, D, C, dt, dc, rot, update_stats);
+        ZF_CHECK_LAUNCH("bn_fwd_small");
+      } else {
+        hipLaunchKernelGGL(zf::gather_u_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, sin, c,
+                           nb.U, B, D, C, dt, dc, rot);
+        ZF_CHECK_LAUNCH("gather_u_kernel");
+        rc = zf_colstats(nb.U, B, DC, DC, 0, nullptr, nullptr, nullptr, nullptr, t->d_dsmall, t->d_dsmall + 128,
+                         t->d_colws, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(128), 0, st, t->d_dsmall, t->d_dsmall + 128, B, DC,
+                           bn, nb.mean, nb.rstd, update_stats);
+        ZF_CHECK_LAUNCH("bn_stats_kernel");
+        hipLaunchKernelGGL(zf::bn_apply_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.U,
+                           nb.mean, nb.rstd, bn + 2 * DC, bn + 3 * DC, nb.Uhat, nb.Ubn, B, DC);
+        ZF_CHECK_LAUNCH("bn_apply_kernel");
+      }
       const float* in = nb.Ubn;
       int in_w = DC;
       for (int l = 0; l <= op.n_hidden; ++l) {
@@ -936,9 +1118,7 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
   ZF_CHECK_LAUNCH("latent_loss_kernel");
   hipLaunchKernelGGL(zf::sum_partials_kernel, dim3(1), dim3(64), 0, st, t->d_part, nblk, t->d_part + nblk);
   ZF_CHECK_LAUNCH("sum_partials_kernel");
-  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, t->d_part + nblk, sizeof(double), hipMemcpyDeviceToDevice, st));
   // ---- reverse ----
-  float* G = grad ? grad : t->d_grad;
   ZF_TRY_HIP(hipMemsetAsync(G, 0, (size_t)t->nat_floats * sizeof(float), st));
   const float gl = -1.0f / (float)B;  // d loss / d log_det of every op and row
   for (int i = desc.n_ops - 1; i >= 0; --i) {
@@ -980,17 +1160,23 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
     // BatchNorm: gU holds d loss / d Ubn
     float* bn = nat + op.off_bn;
     float* gbn = G + op.off_bn;
-    rc = zf::colsum(nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, t->d_ws, st);
-    if (rc) return rc;
-    rc = zf::colsum(nb.gU, nullptr, B, DC, gbn + 3 * DC, t->d_ws, st);
-    if (rc) return rc;
-    // gU := d loss / d U, in place (reads each element before writing it)
-    hipLaunchKernelGGL(zf::bn_bwd_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.gU, nb.Uhat,
-                       bn + 2 * DC, nb.rstd, gbn + 3 * DC, gbn + 2 * DC, nb.gU, B, DC);
-    ZF_CHECK_LAUNCH("bn_bwd_kernel");
-    hipLaunchKernelGGL(zf::scatter_gu_kernel, dim3(zf::blocks_for((int64_t)B * dc)), dim3(256), 0, st, nb.gU, g_prev,
-                       B, D, C, dt, dc, r);
-    ZF_CHECK_LAUNCH("scatter_gu_kernel");
+    if ((long long)B * DC <= zf::kBnSmall) {
+      hipLaunchKernelGGL(zf::bn_bwd_small, dim3(1), dim3(1024), 0, st, nb.gU, nb.Uhat, bn + 2 * DC, nb.rstd,
+                         gbn + 2 * DC, gbn + 3 * DC, g_prev, B, D, C, dt, dc, r);
+      ZF_CHECK_LAUNCH("bn_bwd_small");
+    } else {
+      rc = zf::colsum(nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, t->d_ws, st);
+      if (rc) return rc;
+      rc = zf::colsum(nb.gU, nullptr, B, DC, gbn + 3 * DC, t->d_ws, st);
+      if (rc) return rc;
+      // gU := d loss / d U, in place (reads each element before writing it)
+      hipLaunchKernelGGL(zf::bn_bwd_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.gU,
+                         nb.Uhat, bn + 2 * DC, nb.rstd, gbn + 3 * DC, gbn + 2 * DC, nb.gU, B, DC);
+      ZF_CHECK_LAUNCH("bn_bwd_kernel");
+      hipLaunchKernelGGL(zf::scatter_gu_kernel, dim3(zf::blocks_for((int64_t)B * dc)), dim3(256), 0, st, nb.gU,
+                         g_prev, B, D, C, dt, dc, r);
+      ZF_CHECK_LAUNCH("scatter_gu_kernel");
+    }
     float* tmp = g;
     g = g_prev;
     g_prev = tmp;
@@ -998,20 +1184,80 @@ int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_
   return ZF_OK;
 }
 
-int zf_trainer_step(zf_trainer_t* t, const float* x, const float* c, int64_t B, double* loss, void* stream) {
-  if (!t) return zf::einval("trainer is NULL");
-  int rc = zf_trainer_loss_grad(t, x, c, B, 1, loss, nullptr, stream);
-  if (rc) return rc;
-  t->t += 1;
+int trainer_update(zf_trainer_t* t, hipStream_t st) {
   const zf_optim_desc& o = t->opt;
-  const double tt = (double)t->t;
-  const float bc1 = (float)(1.0 - std::pow((double)o.b1, tt));
-  const float bc1n = (float)(1.0 - std::pow((double)o.b1, tt + 1.0));
-  const float bc2 = (float)(1.0 - std::pow((double)o.b2, tt));
-  hipLaunchKernelGGL(zf::adam_kernel, dim3(zf::blocks_for(t->nat_floats)), dim3(256), 0, (hipStream_t)stream,
-                     t->d_nat, t->d_grad, t->d_m, t->d_v, t->d_mask, (long long)t->nat_floats, o.learning_rate, o.b1,
-                     o.b2, o.eps, o.weight_decay, o.nesterov, bc1, bc1n, bc2);
+  hipLaunchKernelGGL(step_kernel, dim3(1), dim3(1), 0, st, t->d_bc, o.b1, o.b2);
+  ZF_CHECK_LAUNCH("step_kernel");
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, t->d_nat, t->d_grad, t->d_m,
+                     t->d_v, t->d_mask, (long long)t->nat_floats, o.learning_rate, o.b1, o.b2, o.eps, o.weight_decay,
+                     o.nesterov, t->d_bc);
   ZF_CHECK_LAUNCH("adam_kernel");
+  return ZF_OK;
+}
+
+// The whole step (body + optimiser) captured once per batch size.
+int step_graph(zf_trainer_t* t, int B, hipGraphExec_t* out) {
+  auto it = t->graphs.find(B);
+  if (it != t->graphs.end()) {
+    *out = it->second;
+    return ZF_OK;
+  }
+  if (t->graphs.size() >= 8) {  // bound the cache (batch sizes rarely vary)
+    ZF_TRY_HIP(hipStreamSynchronize(t->cap));
+    ZF_TRY_HIP(hipDeviceSynchronize());
+    for (auto& kv : t->graphs) (void)hipGraphExecDestroy(kv.second);
+    t->graphs.clear();
+  }
+  ZF_TRY_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
+  int rc = trainer_body(t, B, 1, t->d_grad, t->cap);
+  if (!rc) rc = trainer_update(t, t->cap);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(t->cap, &g);
+  if (!rc && e != hipSuccess) rc = hip_status(e, "hipStreamEndCapture");
+  hipGraphExec_t exec = nullptr;
+  if (!rc) {
+    const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) rc = hip_status(ei, "hipGraphInstantiate");
+  }
+  if (g) (void)hipGraphDestroy(g);
+  if (rc) return rc;
+  t->graphs[B] = exec;
+  *out = exec;
+  return ZF_OK;
+}
+
+}  // namespace
+}  // namespace zf
+
+extern "C" {
+
+int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_t B, int update_stats,
+                         double* loss, float* grad, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int rc = zf::trainer_stage(t, x, c, B, st);
+  if (rc) return rc;
+  rc = zf::trainer_body(t, (int)B, update_stats, grad ? grad : t->d_grad, st);
+  if (rc) return rc;
+  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t, (int)B), sizeof(double), hipMemcpyDeviceToDevice, st));
+  return ZF_OK;
+}
+
+int zf_trainer_step(zf_trainer_t* t, const float* x, const float* c, int64_t B, double* loss, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int rc = zf::trainer_stage(t, x, c, B, st);
+  if (rc) return rc;
+  if (t->use_graph) {
+    hipGraphExec_t exec = nullptr;
+    rc = zf::step_graph(t, (int)B, &exec);
+    if (rc) return rc;
+    ZF_TRY_HIP(hipGraphLaunch(exec, st));
+  } else {
+    rc = zf::trainer_body(t, (int)B, 1, t->d_grad, st);
+    if (!rc) rc = zf::trainer_update(t, st);
+    if (rc) return rc;
+  }
+  t->t += 1;
+  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t, (int)B), sizeof(double), hipMemcpyDeviceToDevice, st));
   return ZF_OK;
 }
 
