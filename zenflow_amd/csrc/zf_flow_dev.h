@@ -211,7 +211,8 @@ __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, fl
 template <int T>
 __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict__ blob, const float* xs,
                                        const float* __restrict__ cin, long long row, bool valid, int C,
-                                       int rot, int D, int s, int hh, int lane, floatx16 (&hb)[T]) {
+                                       int rot, int D, int s, int hh, int lane, floatx16 (&hb)[T],
+                                       int swish_tiles = T) {
   const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
   const int DCp = 2 * KS0;
   const float* bn = blob + op.bn;
@@ -228,10 +229,13 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
     for (int o = 0; o < T; ++o)
       hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
   }
+  // swish of tiles [0, swish_tiles): the bf16x3 kernel defers the others into
+  // the next layer's MFMA stream
 #pragma unroll
   for (int o = 0; o < T; ++o)
+    if (o < swish_tiles)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
+      for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
 }
 
 // latent.log_prob(z) + log_det, nan_to_num (flow.py:41-48;

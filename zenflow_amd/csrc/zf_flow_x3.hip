@@ -42,6 +42,14 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// Hidden 256 (one wave per SIMD, nothing else to hide LDS latency or fill
+// MFMA issue gaps): A fragments one output tile ahead, and each group's
+// MFMAs interleaved with its VALU by sched_group_barrier (measured +4-5% at
+// cfg5; at T = 4 both were neutral to -12% and stay off).
+#ifndef ZF_X3_WIDE_SCHED
+#define ZF_X3_WIDE_SCHED 3
+#endif
+
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
 constexpr int group_bytes(int NOUT) { return 2 * NOUT * 3 * 1024; }
@@ -106,6 +114,35 @@ template <int T, int NOUT, int Q>
 __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
                                          int lane) {
   const char* lb = buf + lane * 16;
+if constexpr (T == 8) {
+  // A fragments one output tile ahead (LDS latency off the MFMA chain).
+  auto frag = [&](int t, bf16x8& ah, bf16x8& am, bf16x8& al) {
+    const char* a = lb + ((t * 3) << 10);
+    am = *reinterpret_cast<const bf16x8*>(a + 1024);
+    ah = *reinterpret_cast<const bf16x8*>(a);
+    al = *reinterpret_cast<const bf16x8*>(a + 2048);
+  };
+  bf16x8 ch, cm, cl;
+  frag(0, ch, cm, cl);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 bh, bm, bl;
+    if (s == 0) split8<0>(hb[Q], bh, bm, bl);
+    else split8<1>(hb[Q], bh, bm, bl);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      const int t = s * NOUT + o;
+      bf16x8 nh, nm, nl;
+      if (t + 1 < 2 * NOUT) frag(t + 1, nh, nm, nl);
+      acc[o] = mfma3(ch, cm, cl, bh, bm, bl, acc[o]);
+      if (t + 1 < 2 * NOUT) {
+        ch = nh;
+        cm = nm;
+        cl = nl;
+      }
+    }
+  }
+} else {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     bf16x8 bh, bm, bl;
@@ -114,12 +151,13 @@ __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
       const char* a = lb + (((s * NOUT + o) * 3) << 10);
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
       const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
       const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
       acc[o] = mfma3(ah, am, al, bh, bm, bl, acc[o]);
     }
   }
+}
 }
 
 // The group stream of the NSC being computed (byte offsets into the x3
@@ -205,8 +243,8 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
 // group into it, then this group's MFMAs.  `bias` (optional): bias tiles of
 // a layer that started from zero, loaded here — in the layer's last step,
 // when its earlier input tiles are dead — and added after the MFMAs.
-template <int T, int NOUT, int Q>
-__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[T],
+template <int T, int NOUT, int Q, bool SW>
+__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
                                         int hh) {
   constexpr int kBuf = group_bytes(T);
@@ -225,20 +263,39 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   } else {
     x3_group<T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
   }
+  // SW: the layer input arrives as pre-activations except tile 0; the swish
+  // of tile Q+1 goes here, in the same scheduling region as this group's
+  // MFMAs, whose issue gaps it fills.
+  if constexpr (SW && Q + 1 < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = swish(hb[Q + 1][r]);
+  }
+  if constexpr (T == 8 && ZF_X3_WIDE_SCHED > 0) {
+    // the k-step-0 split first, then every MFMA followed by its share of LDS
+    // reads and VALU (split of k-step 1, the deferred swish)
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    __builtin_amdgcn_sched_group_barrier(0x402, 20, 0);
+#pragma unroll
+    for (int i = 0; i < 12 * NOUT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_WIDE_SCHED, 0);
+    }
+  }
   p.buf ^= 1;
   p.g += 1;
 }
 
 // A whole streamed Dense layer: T groups (one per input tile).
-template <int T, int NOUT, int Q = 0>
-__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, const floatx16 (&hb)[T],
+template <int T, int NOUT, bool SW, int Q = 0>
+__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                          floatx16 (&acc)[NOUT], int lane, const float* bias_last = nullptr,
                                          int hh = 0) {
   if constexpr (Q + 1 < T) {
-    x3_step<T, NOUT, Q>(x3, p, hb, acc, lane, nullptr, hh);
-    x3_layer<T, NOUT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
+    x3_step<T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh);
+    x3_layer<T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
   } else {
-    x3_step<T, NOUT, Q>(x3, p, hb, acc, lane, bias_last, hh);
+    x3_step<T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh);
   }
 }
 
@@ -318,7 +375,12 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
       pipe.g = 0;
       floatx16 hb[T];
       X3_MARK(3);
-      layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
+      // The swish of a layer's output is deferred tile by tile into the next
+      // streamed layer (x3_step, SW) — except before a PAIRS last layer,
+      // which passes over its input once per dim pair.
+      constexpr bool kLastSW = !PAIRS;
+      layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
+                (op.n_hidden > 1 || kLastSW) ? 1 : T);
       X3_MARK(4);
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each; the biases
       // seed the accumulators.
@@ -326,12 +388,18 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
         floatx16 acc[T];
 #pragma unroll
         for (int o = 0; o < T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
-        x3_layer<T, T>(x3, pipe, hb, acc, lane);
+        x3_layer<T, T, true>(x3, pipe, hb, acc, lane);
         X3_MARK(5);
+        const int nsw = (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
 #pragma unroll
-        for (int o = 0; o < T; ++o)
+        for (int o = 0; o < T; ++o) {
+          if (o < nsw) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
+            for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
+          } else {
+            hb[o] = acc[o];
+          }
+        }
       }
       // Last Dense (:346-347), one pair of transformed dims at a time: lane
       // half h, tile o, register r = parameter 16*o + r of dim 2*pair + h.
@@ -349,7 +417,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
 #pragma unroll
         for (int o = 0; o < TL; ++o) pa[o] = PAIRS ? bias_acc(bl + o * 32, hh) : floatx16{0};
         X3_MARK(6);
-        x3_layer<T, TL>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
+        x3_layer<T, TL, kLastSW>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
         X3_MARK(7);
         float P[TL * 16];
 #pragma unroll
