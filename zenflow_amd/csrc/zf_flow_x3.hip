@@ -286,6 +286,87 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   p.g += 1;
 }
 
+// k-step-level software pipeline (hidden 128, one pass per layer): group Q
+// multiplies k-step (Q, 0) with the split carried in `cs`, and beside its
+// MFMAs forms the split of (Q, 1), the swish of tile Q+1 and the split of
+// (Q+1, 0) for the next group — so the bf16 split and the deferred swish sit
+// in the MFMA issue gaps of the same wave (cross-wave they would not overlap:
+// tests/hip/coexec_probe.hip modes 2 and 6).
+#ifndef ZF_X3_PIPE
+#define ZF_X3_PIPE 1
+#endif
+#ifndef ZF_X3_PIPE_VALU
+#define ZF_X3_PIPE_VALU 0
+#endif
+template <int T, int NOUT, int Q, bool HASB>
+__device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                             floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                             int hh, bf16x8 (&cs)[3]) {
+  constexpr int kBuf = group_bytes(T);
+  X3_MARK(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  X3_MARK(2);
+  x3_issue_next<T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
+  floatx16 bt[NOUT];
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+  }
+  const char* lb = p.wbuf + p.buf * kBuf + lane * 16;
+  bf16x8 s1[3];
+  split8<1>(hb[Q], s1[0], s1[1], s1[2]);
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    const char* a = lb + ((o * 3) << 10);
+    const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
+    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
+    const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
+    acc[o] = mfma3(ah, am, al, cs[0], cs[1], cs[2], acc[o]);
+  }
+  if constexpr (Q + 1 < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = swish(hb[Q + 1][r]);
+    split8<0>(hb[Q + 1], cs[0], cs[1], cs[2]);
+  }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    const char* a = lb + (((NOUT + o) * 3) << 10);
+    const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
+    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
+    const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
+    acc[o] = mfma3(ah, am, al, s1[0], s1[1], s1[2], acc[o]);
+  }
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] += bt[o];
+  }
+#if ZF_X3_PIPE_VALU > 0
+  __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+  for (int i = 0; i < 12 * NOUT; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_PIPE_VALU, 0);
+  }
+#endif
+  p.buf ^= 1;
+  p.g += 1;
+}
+
+// A pipelined layer: hb[0] already swished, cs = split of (0, 0).
+template <int T, int NOUT, bool HASB, int Q = 0>
+__device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                              floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
+                                              bf16x8 (&cs)[3]) {
+  if constexpr (Q + 1 < T) {
+    x3_step_pipe<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs);
+    x3_layer_pipe<T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs);
+  } else {
+    x3_step_pipe<T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs);
+  }
+}
+
 // A whole streamed Dense layer: T groups (one per input tile).
 template <int T, int NOUT, bool SW, int Q = 0>
 __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
@@ -316,7 +397,10 @@ __device__ __forceinline__ float squareplus_rsq(float x) {
 // SIMD, <= 168 VGPRs), 104 KiB at T = 8 (hidden 256: one block per CU, the
 // 8 + 8 accumulator tiles need one wave's whole register file).
 template <int K, int T, bool PAIRS, bool INV>
-__global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
+#ifndef ZF_X3_NARROW_OCC
+#define ZF_X3_NARROW_OCC 3
+#endif
+__global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
@@ -379,6 +463,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
       // streamed layer (x3_step, SW) — except before a PAIRS last layer,
       // which passes over its input once per dim pair.
       constexpr bool kLastSW = !PAIRS;
+      constexpr bool kPipe = T == 4 && !PAIRS && ZF_X3_PIPE;
       layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
                 (op.n_hidden > 1 || kLastSW) ? 1 : T);
       X3_MARK(4);
@@ -388,7 +473,13 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
         floatx16 acc[T];
 #pragma unroll
         for (int o = 0; o < T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
-        x3_layer<T, T, true>(x3, pipe, hb, acc, lane);
+        if constexpr (kPipe) {
+          bf16x8 cs[3];
+          split8<0>(hb[0], cs[0], cs[1], cs[2]);
+          x3_layer_pipe<T, T, false>(x3, pipe, hb, acc, lane, nullptr, hh, cs);
+        } else {
+          x3_layer<T, T, true>(x3, pipe, hb, acc, lane);
+        }
         X3_MARK(5);
         const int nsw = (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
 #pragma unroll
@@ -417,7 +508,13 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? 3 : 1) void flow_kernel_x3(
 #pragma unroll
         for (int o = 0; o < TL; ++o) pa[o] = PAIRS ? bias_acc(bl + o * 32, hh) : floatx16{0};
         X3_MARK(6);
-        x3_layer<T, TL, kLastSW>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
+        if constexpr (kPipe) {
+          bf16x8 cs[3];
+          split8<0>(hb[0], cs[0], cs[1], cs[2]);
+          x3_layer_pipe<T, TL, true>(x3, pipe, hb, pa, lane, bl, hh, cs);
+        } else {
+          x3_layer<T, TL, kLastSW>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
+        }
         X3_MARK(7);
         float P[TL * 16];
 #pragma unroll
