@@ -110,14 +110,22 @@ def spline_kernel_roofline(M, N, K, steps):
     dx = DeviceArray.from_numpy(rng.standard_normal((M, N, K)).astype(np.float32))
     dy = DeviceArray.from_numpy(rng.standard_normal((M, N, K)).astype(np.float32))
     sl = DeviceArray.from_numpy(rng.standard_normal((M, N, K - 1)).astype(np.float32))
+    # utils.normalize_spline_params on copies of the raw logits (in place;
+    # repeated runs stay finite), then once on the K1 inputs themselves
+    cdx, cdy, csl = DeviceArray(dx.shape), DeviceArray(dy.shape), DeviceArray(sl.shape)
+    cdx.copy_from(dx)
+    cdy.copy_from(dy)
+    csl.copy_from(sl)
     L.check(lib.zf_normalize_spline_params(dx.ptr, dy.ptr, sl.ptr, M * N, K, L.stream()), "normalize")
     y = DeviceArray((M, N))
     ld = DeviceArray((M,))
     xi = DeviceArray((M, N))
     out = {}
-    for tag in ("forward", "inverse"):
+    for tag in ("forward", "inverse", "normalize"):
         def run():
-            if tag == "forward":
+            if tag == "normalize":
+                L.check(lib.zf_normalize_spline_params(cdx.ptr, cdy.ptr, csl.ptr, M * N, K, L.stream()), "normalize")
+            elif tag == "forward":
                 L.check(lib.zf_rqs_forward(x.ptr, dx.ptr, dy.ptr, sl.ptr, y.ptr, ld.ptr, M, N, K, L.stream()), "rqs")
             else:
                 L.check(lib.zf_rqs_inverse(y.ptr, dx.ptr, dy.ptr, sl.ptr, xi.ptr, M, N, K, L.stream()), "rqs")
@@ -130,9 +138,14 @@ def spline_kernel_roofline(M, N, K, steps):
             b.record()
         L.synchronize()
         t = float(np.mean([a.elapsed_ms(b) for a, b in evs])) * 1e-3
-        nbytes = M * (N * (4 * 3 * K + 4) + (4 if tag == "forward" else 0))
+        if tag == "normalize":  # read + write dx, dy, slope
+            nbytes = 2 * M * N * 4 * (3 * K - 1)
+            kname = "normalize_kernel"
+        else:
+            nbytes = M * (N * (4 * 3 * K + 4) + (4 if tag == "forward" else 0))
+            kname = "rqs_kernel_direct" if K in (4, 8, 16, 32) else "rqs_kernel"
         gbs = nbytes / t / 1e9
-        out[tag] = {"kernel": "rqs_kernel", "shape": [M, N, K], "us": t * 1e6, "alg_bytes": nbytes,
+        out[tag] = {"kernel": kname, "shape": [M, N, K], "us": t * 1e6, "alg_bytes": nbytes,
                     "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
     return out
 

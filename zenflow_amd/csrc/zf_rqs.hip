@@ -166,23 +166,73 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
   }
 }
 
-// utils.py:23-34, 37-62 — one thread per row.
-__global__ void normalize_kernel(float* __restrict__ dx, float* __restrict__ dy,
-                                 float* __restrict__ sl, int64_t M, int K) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
+// Row-wise utils kernels (thresholded softmax, normalize_spline_params):
+// one thread per row, but the block's rows (contiguous in HBM) are staged
+// through LDS with coalesced loads and stores (odd row stride) — a thread
+// walking its own row in global memory would touch a new cache line per
+// element and re-read each row once per pass.
+constexpr int kRowThreads = 256;
+constexpr int kRowLdsFloats = 12288;  // 48 KiB budget per block (dynamic, sized to the rows)
+
+__host__ __device__ inline int row_stride(int K) { return K | 1; }
+inline int rows_per_block(int K) {
+  const int r = kRowLdsFloats / row_stride(K);
+  return r < kRowThreads ? r : kRowThreads;
+}
+
+__device__ __forceinline__ void rows_in(float* lds, const float* __restrict__ src, int rows, int K) {
+  const int ks = row_stride(K), n = rows * K;
+  for (int e = threadIdx.x; e < n; e += kRowThreads) {
+    const int r = e / K;
+    lds[r * ks + (e - r * K)] = src[e];
+  }
+}
+
+__device__ __forceinline__ void rows_out(float* __restrict__ dst, const float* lds, int rows, int K) {
+  const int ks = row_stride(K), n = rows * K;
+  for (int e = threadIdx.x; e < n; e += kRowThreads) {
+    const int r = e / K;
+    dst[e] = lds[r * ks + (e - r * K)];
+  }
+}
+
+// (squareplus(v) / sum + c) / norm over a row in LDS (utils.py:23-34).
+__device__ __forceinline__ void softmax_row(float* r, int K, float c, float norm) {
+  float xs = 0.f;
+  for (int j = 0; j < K; ++j) {
+    const float v = squareplus(r[j]);
+    r[j] = v;
+    xs = xs + v;
+  }
+  for (int j = 0; j < K; ++j) r[j] = (r[j] / xs + c) / norm;
+}
+
+// utils.py:37-62: dx, dy rows through softmax_with_threshold, slopes through
+// squareplus (elementwise over the block's contiguous slope rows).
+__global__ __launch_bounds__(kRowThreads) void normalize_kernel(float* __restrict__ dx, float* __restrict__ dy,
+                                                                float* __restrict__ sl, int64_t M, int K, int R) {
+  extern __shared__ float lds[];  // [2][R][row_stride(K)]: dx and dy rows together
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)(M - r0 < R ? M - r0 : R);
   const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // Python floats (utils.py:32)
   const float c = (float)c64;
   const float norm = (float)(1.0 + c64 * (double)K);
-  float* rows[2] = {dx + m * K, dy + m * K};
-  for (int a = 0; a < 2; ++a) {
-    float* r = rows[a];
-    float xs = 0.f;
-    for (int j = 0; j < K; ++j) { const float s = squareplus(r[j]); r[j] = s; xs = xs + s; }
-    for (int j = 0; j < K; ++j) r[j] = (r[j] / xs + c) / norm;
+  float* ly = lds + R * row_stride(K);
+  rows_in(lds, dx + r0 * K, rows, K);
+  rows_in(ly, dy + r0 * K, rows, K);
+  __syncthreads();
+  if ((int)threadIdx.x < rows) {
+    softmax_row(lds + threadIdx.x * row_stride(K), K, c, norm);
+    softmax_row(ly + threadIdx.x * row_stride(K), K, c, norm);
   }
-  float* s = sl + m * (K - 1);
-  for (int j = 0; j < K - 1; ++j) s[j] = squareplus(s[j]);
+  __syncthreads();
+  rows_out(dx + r0 * K, lds, rows, K);
+  rows_out(dy + r0 * K, ly, rows, K);
+  if (K > 1) {
+    float* s = sl + r0 * (K - 1);
+    const int n = rows * (K - 1);
+    for (int e = threadIdx.x; e < n; e += kRowThreads) s[e] = squareplus(s[e]);
+  }
 }
 
 // utils.py:18-20 elementwise; b is the reference's `b` argument.
@@ -193,15 +243,17 @@ __global__ void squareplus_kernel(const float* __restrict__ x, float* __restrict
 }
 
 // utils.py:23-34 over rows of K; c and 1 + c*n are float64 Python scalars.
-__global__ void softmax_threshold_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                         int64_t M, int K, float c, float norm) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  const float* r = x + m * K;
-  float* o = y + m * K;
-  float xs = 0.f;
-  for (int j = 0; j < K; ++j) xs = xs + squareplus(r[j]);
-  for (int j = 0; j < K; ++j) o[j] = (squareplus(r[j]) / xs + c) / norm;
+__global__ __launch_bounds__(kRowThreads) void softmax_threshold_kernel(const float* __restrict__ x,
+                                                                        float* __restrict__ y, int64_t M, int K,
+                                                                        int R, float c, float norm) {
+  extern __shared__ float lds[];  // [R][row_stride(K)]
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)(M - r0 < R ? M - r0 : R);
+  rows_in(lds, x + r0 * K, rows, K);
+  __syncthreads();
+  if ((int)threadIdx.x < rows) softmax_row(lds + threadIdx.x * row_stride(K), K, c, norm);
+  __syncthreads();
+  rows_out(y + r0 * K, lds, rows, K);
 }
 
 template <bool FWD>
@@ -284,10 +336,14 @@ int zf_softmax_with_threshold(const float* x, float* y, int64_t M, int K, double
   if (M < 0 || K < 1) return zf::einval("bad shape");
   if (M == 0) return ZF_OK;
   if (!x || !y) return zf::einval("NULL argument");
+  if (K > zf::kRowLdsFloats / 2) return zf::einval("K too large");
   const double c64 = threshold / (1.0 - (double)K * threshold);
-  const int64_t grid = (M + 255) / 256;
-  hipLaunchKernelGGL(zf::softmax_threshold_kernel, dim3((unsigned)grid), dim3(256), 0,
-                     (hipStream_t)stream, x, y, M, K, (float)c64, (float)(1.0 + c64 * (double)K));
+  const int R = zf::rows_per_block(K);
+  const int64_t grid = (M + R - 1) / R;
+  if (grid > 0x7fffffffLL) return zf::einval("M too large");
+  hipLaunchKernelGGL(zf::softmax_threshold_kernel, dim3((unsigned)grid), dim3(zf::kRowThreads),
+                     (size_t)R * zf::row_stride(K) * sizeof(float),
+                     (hipStream_t)stream, x, y, M, K, R, (float)c64, (float)(1.0 + c64 * (double)K));
   ZF_CHECK_LAUNCH("softmax_threshold_kernel");
   return ZF_OK;
 }
@@ -297,10 +353,13 @@ int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, in
   if (M < 0 || K < 1) return zf::einval("bad shape");
   if (M == 0) return ZF_OK;
   if (!dx || !dy || (K > 1 && !slope)) return zf::einval("NULL input");
-  const int threads = 256;
-  const int64_t grid = (M + threads - 1) / threads;
-  hipLaunchKernelGGL(zf::normalize_kernel, dim3((unsigned)grid), dim3(threads), 0,
-                     (hipStream_t)stream, dx, dy, slope, M, K);
+  if (K > zf::kRowLdsFloats / 2) return zf::einval("K too large");
+  const int R = zf::rows_per_block(2 * K + 1);  // dx and dy rows share the LDS budget
+  const int64_t grid = (M + R - 1) / R;
+  if (grid > 0x7fffffffLL) return zf::einval("M too large");
+  hipLaunchKernelGGL(zf::normalize_kernel, dim3((unsigned)grid), dim3(zf::kRowThreads),
+                     (size_t)2 * R * zf::row_stride(K) * sizeof(float),
+                     (hipStream_t)stream, dx, dy, slope, M, K, R);
   ZF_CHECK_LAUNCH("normalize_kernel");
   return ZF_OK;
 }
