@@ -11,6 +11,7 @@ import hashlib
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
@@ -21,7 +22,7 @@ ARCH = os.environ.get("ZF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["zf_runtime.hip", "zf_rqs.hip", "zf_flow.hip", "zf_flow_x3.hip", "zf_stats.hip", "zf_rccl.hip", "zf_train.hip"]
-HEADERS = ["zf_internal.h", "zf_spline.h"]
+HEADERS = sorted(p.name for p in CSRC.glob("*.h"))
 
 FLAGS = [
     f"--offload-arch={ARCH}",
@@ -54,7 +55,23 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and LIB.exists() and stamp.exists() and stamp.read_text() == fp:
         return LIB
     tmp = LIB.with_suffix(".so.tmp")
-    cmd = [HIPCC, *FLAGS, "-o", str(tmp), *[str(CSRC / s) for s in SOURCES], "-ldl"]
+    objdir = HERE.parent / "build" / "obj"
+    objdir.mkdir(parents=True, exist_ok=True)
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+
+    def _compile(src: str) -> Path:
+        obj = objdir / (Path(src).stem + ".o")
+        cmd = [HIPCC, *compile_flags, "-c", "-o", str(obj), str(CSRC / src)]
+        if verbose:
+            print("[zenflow_amd.build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    # one hipcc per translation unit, in parallel (the kernels dominate build time)
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(jobs) as pool:
+        objs = list(pool.map(_compile, SOURCES))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), "-ldl"]
     if verbose:
         print("[zenflow_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
