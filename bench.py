@@ -29,6 +29,12 @@ PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (no xf32 o
 PEAK_BF16_MFMA_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz
 # fp32-accurate GEMM by the three-term bf16 split: 6 bf16 products per fp32 product
 PEAK_BF16X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+# two-term fp16 split of power-of-two-scaled operands: 3 fp16 products (fp16 dense = bf16 dense rate)
+PEAK_F16X2_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
+SPLIT_PEAKS = {
+    "bf16x3": (PEAK_BF16X3_TFLOPS, "bf16 dense MFMA peak / 6 (three-term bf16 split, fp32-equivalent flops)"),
+    "f16x2": (PEAK_F16X2_TFLOPS, "fp16 dense MFMA peak / 3 (two-term fp16 split, fp32-equivalent flops)"),
+}
 PEAK_HBM_GBS = 8000.0
 
 WORKLOADS = {
@@ -295,8 +301,8 @@ def main():
     fps = flops_per_sample(name)
     achieved = fps * N / (kavg * 1e-3) / 1e12
     variant = prog.kernel_variant
-    kernel_name = "flow_kernel_x3" if variant == "bf16x3" else "flow_kernel"
-    peak = PEAK_BF16X3_TFLOPS if variant == "bf16x3" else PEAK_FP32_MFMA_TFLOPS
+    kernel_name = "flow_kernel_x3" if variant in SPLIT_PEAKS else "flow_kernel"
+    peak, peak_basis = SPLIT_PEAKS.get(variant, (PEAK_FP32_MFMA_TFLOPS, "fp32 dense MFMA peak"))
     traffic = load_traffic(kernel_name, 1)
     result = {
         "metric": "log_prob samples/sec (+ NLL match) 4D 16-knot 4-layer flow, batch 2^20"
@@ -331,8 +337,7 @@ def main():
             "traffic": traffic,
             "kernel": f"{kernel_name} (avg {kavg * 1e3:.1f} us over {args.steps} timed launches, HIP events)",
             "alg_flops_per_sample": fps,
-            "peak_basis": "bf16 dense MFMA peak / 6 (three-term split, fp32-equivalent flops)"
-            if variant == "bf16x3" else "fp32 dense MFMA peak",
+            "peak_basis": peak_basis,
             "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
         },
     }

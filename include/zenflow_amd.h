@@ -160,12 +160,17 @@ int zf_flow_destroy(zf_flow_t* handle);
 
 /* Which fused kernel the handle runs (no reference counterpart: an
  * implementation detail made observable for tests and benchmarks):
- * ZF_KERNEL_FP32 (fp32 MFMA, any supported shape) or ZF_KERNEL_BF16X3
- * (three-term bf16 split on bf16 MFMA, fp32-equivalent accuracy; hidden
- * widths <= 128 padded to 128, knots 8 or 16, dim <= 5; disabled by the
- * environment variable ZF_DISABLE_X3=1 at zf_flow_create time).  -1 if h is NULL. */
+ * ZF_KERNEL_FP32 (fp32 MFMA, any supported shape), or the split-MFMA kernel
+ * for the shapes it covers (hidden widths <= 128 with knots 8/16 and dim <= 5;
+ * hidden <= 256 with knots 16/32 and dim <= 17) in one of two schemes:
+ * ZF_KERNEL_F16X2 (default: two-term fp16 split of power-of-two-scaled
+ * operands, three fp16 MFMAs per k-step) or ZF_KERNEL_BF16X3 (three-term
+ * bf16 split, six bf16 MFMAs per k-step; ZF_X3_SCHEME=bf16x3).  The
+ * environment is read at zf_flow_create time; ZF_DISABLE_X3=1 forces
+ * ZF_KERNEL_FP32.  -1 if h is NULL. */
 #define ZF_KERNEL_FP32 0
 #define ZF_KERNEL_BF16X3 1
+#define ZF_KERNEL_F16X2 2
 int zf_flow_kernel_variant(const zf_flow_t* h);
 
 /* Device workspace needed by zf_flow_log_prob for N rows. */

@@ -198,19 +198,23 @@ def test_edge_inputs():
 
 
 # --- kernel variants -----------------------------------------------------------
-# Shapes the bf16x3 kernel takes (hidden <= 128 with knots 8/16 and dim <= 5;
-# hidden 256 with knots 16/32 and dim <= 17) run on it by default; ZF_DISABLE_X3=1 forces the fp32-MFMA kernel, which must stay
-# parity-green on the same shapes.
+# Shapes the split-MFMA kernel takes (hidden <= 128 with knots 8/16 and dim <= 5;
+# hidden 256 with knots 16/32 and dim <= 17) run on it by default, in the f16x2
+# scheme; ZF_X3_SCHEME=bf16x3 selects the three-term bf16 scheme and
+# ZF_DISABLE_X3=1 the fp32-MFMA kernel, which must stay parity-green on the
+# same shapes.
 
 X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5"]
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"])
-def test_kernel_selection(name):
+def test_kernel_selection(name, monkeypatch):
     case = make_case(name, N=8, seed=30)
     _, bf = _bound(case)
-    want = "bf16x3" if name in X3_SHAPES else "fp32"
-    assert bf.program.kernel_variant == want
+    assert bf.program.kernel_variant == ("f16x2" if name in X3_SHAPES else "fp32")
+    monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == ("bf16x3" if name in X3_SHAPES else "fp32")
 
 
 @pytest.mark.parametrize("name", X3_SHAPES)
@@ -222,15 +226,55 @@ def test_fp32_kernel_parity_when_x3_disabled(name, monkeypatch):
     check_lp(gpu_log_prob(case), case, f"fp32/{name}")
 
 
+@pytest.mark.parametrize("name", X3_SHAPES)
+def test_bf16x3_scheme_parity(name, monkeypatch):
+    monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
+    case = make_case(name, N=3000, seed=34)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "bf16x3"
+    check_lp(gpu_log_prob(case), case, f"bf16x3/{name}")
+
+
+@pytest.mark.parametrize("scheme", ["f16x2", "bf16x3"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg5"])
+@pytest.mark.parametrize("regime", ["huge_activations", "tiny_activations", "tiny_weights", "huge_weights"])
+def test_split_scaling_extremes(scheme, name, regime, monkeypatch):
+    """f16x2 scales weights per layer and activations per sample by powers of
+    two into fp16's range: parity must not depend on the magnitudes (hidden
+    values ~1e4 overflow unscaled fp16; ~1e-6 fall into its subnormals)."""
+    monkeypatch.setenv("ZF_X3_SCHEME", scheme)
+    case = make_case(name, N=1500, seed=35)
+    params = case["variables"]["params"]["bijector"]
+    for key, p in params.items():
+        if "Dense_1" not in p:
+            continue
+        if regime == "huge_activations":  # BatchNorm output and first Dense scaled up
+            p["BatchNorm_0"]["scale"] = (p["BatchNorm_0"]["scale"] * 3e3).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-3).astype(F32)
+        elif regime == "tiny_activations":
+            p["Dense_0"]["kernel"] = (p["Dense_0"]["kernel"] * 1e-6).astype(F32)
+            p["Dense_0"]["bias"] = (p["Dense_0"]["bias"] * 1e-6).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e4).astype(F32)
+        elif regime == "tiny_weights":
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-7).astype(F32)
+        else:
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e5).astype(F32)
+            last = f"Dense_{len(case['cfg']['layers'])}"
+            p[last]["kernel"] = (p[last]["kernel"] * 1e-5).astype(F32)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == scheme
+    check_lp(gpu_log_prob(case), case, f"{scheme}/{name}/{regime}")
+
+
 @pytest.mark.parametrize("N", [255, 256, 257, 129, 100003])
 def test_x3_ragged_batches(N):
-    """Block = 256 samples on the bf16x3 kernel: partial blocks, the NLL
+    """Block = 128 samples on the split-MFMA kernel: partial blocks, the NLL
     workspace layout shared with the 128-row fp32 kernel."""
     from zenflow_amd._lib import DeviceArray
 
     case = make_case("cfg2", N=N, seed=32)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == "bf16x3"
+    assert bf.program.kernel_variant == "f16x2"
     xd = DeviceArray.from_numpy(case["x"])
     nll = DeviceArray((1,), np.float64)
     lp = bf.log_prob(xd, nll_sum=nll).numpy()

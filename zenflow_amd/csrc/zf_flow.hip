@@ -582,9 +582,10 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
     }
   }
   std::vector<uint16_t> x3s;
-  if (x3 && zf::x3_lds_bytes(T, desc.dim) <= 160 * 1024) {
-    zf::x3_pack(desc, nat, T, F, P, x3s);
-    F.x3_ok = 1;
+  const int NT = zf::x3_scheme();
+  if (x3 && zf::x3_lds_bytes(T, desc.dim, NT) <= 160 * 1024) {
+    zf::x3_pack(desc, nat, T, NT, F, P, x3s);
+    F.x3_ok = NT == 3 ? 1 : 2;
     h->x3_K = x3K;
   }
   const bool use_x3 = F.x3_ok != 0;
@@ -618,7 +619,7 @@ int zf_flow_destroy(zf_flow_t* h) {
 
 int zf_flow_kernel_variant(const zf_flow_t* h) {
   if (!h) return -1;
-  return h->host.x3_ok ? ZF_KERNEL_BF16X3 : ZF_KERNEL_FP32;
+  return h->host.x3_ok == 2 ? ZF_KERNEL_F16X2 : h->host.x3_ok ? ZF_KERNEL_BF16X3 : ZF_KERNEL_FP32;
 }
 
 int64_t zf_flow_workspace_bytes(int64_t N) {
@@ -647,6 +648,7 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.x = x; a.c = c; a.y = y; a.ld_in = ld_in; a.ld_out = ld_out; a.lp = lp; a.part = part;
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
     a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.T = h->host.HP / 32;
+    a.NT = h->host.x3_ok == 2 ? 2 : 3;
     a.seed = seed;
     a.gen = gen;
     a.stream = (hipStream_t)stream;

@@ -35,6 +35,7 @@ struct DevOp {
   long long x3_blast;
   int x3_groups, x3_tlast;
   int x3_next[2];
+  int x3_kw[17];  // f16x2: power-of-two weight scale of streamed layer l (1..n_hidden)
 };
 
 struct DevFlow {
@@ -321,14 +322,16 @@ struct X3Launch {
   unsigned long long seed;
   int gen;  // 1: draw the input rows from the latent (zf_flow_sample)
   int K, D, T;  // knots, dim, hidden tiles (4: width <= 128, 8: <= 256)
+  int NT;       // split scheme: 3 = bf16x3, 2 = f16x2
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
 int x3_pairs(const zf_flow_desc& desc);
-size_t x3_lds_bytes(int T, int D);
-void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, float* packed,
+size_t x3_lds_bytes(int T, int D, int NT);
+int x3_scheme();
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);
 
 }  // namespace zf

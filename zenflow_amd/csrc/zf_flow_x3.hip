@@ -30,6 +30,7 @@
 // ZF_DISABLE_X3=1, runs flow_kernel.
 #include "zf_flow_dev.h"
 
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -41,6 +42,30 @@ namespace {
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+// Split scheme (NT = terms per operand):
+//   NT = 3 "bf16x3": x = hi + mid + lo (RNE bf16 each), six products per
+//          k-step — an fp32 dot product to ~1e-7 relative;
+//   NT = 2 "f16x2":  x*2^k = hi + lo (RNE fp16 each; 11-bit significands, so
+//          the pair holds 22 bits) with hi*hi + hi*lo + lo*hi — three
+//          products, each within ~2^-22 relative.  Operands are scaled by
+//          powers of two into fp16's range: weights per layer on the host
+//          (max |W| * 2^kw in [2^13, 2^14)), activations per sample in the
+//          kernel (x3_act_scale); the accumulator is scaled back exactly.
+template <int NT>
+struct XT;
+template <>
+struct XT<3> {
+  using E = bf16x8;
+  static constexpr int kProd = 6;
+};
+template <>
+struct XT<2> {
+  using E = halfx8;
+  static constexpr int kProd = 3;
+};
 
 // Hidden 256 (one wave per SIMD, nothing else to hide LDS latency or fill
 // MFMA issue gaps): A fragments one output tile ahead, and each group's
@@ -52,7 +77,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
-constexpr int group_bytes(int NOUT) { return 2 * NOUT * 3 * 1024; }
+template <int NT>
+constexpr int group_bytes(int NOUT) { return 2 * NOUT * NT * 1024; }
 
 #ifndef ZF_X3_TRACE
 #define ZF_X3_TRACE 0
@@ -96,6 +122,30 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
   }
 }
 
+// Regs 8s..8s+7 of an accumulator tile, scaled by sc (a power of two) -> hi /
+// lo fp16x8 (RNE each; the residual x*sc - hi is exact).
+template <int S>
+__device__ __forceinline__ void split8h(const floatx16& v, float sc, halfx8& bh, halfx8& bl) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]} * sc;
+    const halfx2 h = __builtin_convertvector(x, halfx2);
+    const floatx2 r = x - __builtin_convertvector(h, floatx2);
+    const halfx2 l = __builtin_convertvector(r, halfx2);
+    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
+    bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
+  }
+}
+
+template <int NT, int S>
+__device__ __forceinline__ void splitk(const floatx16& v, float sc, typename XT<NT>::E (&b)[NT]) {
+  if constexpr (NT == 3) {
+    split8<S>(v, b[0], b[1], b[2]);
+  } else {
+    split8h<S>(v, sc, b[0], b[1]);
+  }
+}
+
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
                                           floatx16 acc) {
@@ -107,54 +157,103 @@ __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, co
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
+// One k-step of the split product, small terms first.
+template <int NT>
+__device__ __forceinline__ floatx16 mfma_split(const typename XT<NT>::E (&a)[NT], const typename XT<NT>::E (&b)[NT],
+                                               floatx16 acc) {
+  if constexpr (NT == 3) {
+    return mfma3(a[0], a[1], a[2], b[0], b[1], b[2], acc);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
+  }
+}
+
+// A fragment (NT parts of 1 KiB; this lane's 16 bytes of each) from LDS.
+template <int NT>
+__device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)[NT]) {
+  using E = typename XT<NT>::E;
+  if constexpr (NT == 3) f[1] = *reinterpret_cast<const E*>(a + 1024);
+  f[0] = *reinterpret_cast<const E*>(a);
+  if constexpr (NT == 3) f[2] = *reinterpret_cast<const E*>(a + 2048);
+  else f[1] = *reinterpret_cast<const E*>(a + 1024);
+}
+
+// f16x2: per-sample power-of-two scale of a layer input so its largest
+// |value| lands in [2^13, 2^14) (|swish(v)| <= |v|, so raw pre-activations
+// of deferred tiles bound their swish), and the exact factor that undoes
+// both scales on the accumulator: us = 2^-(e_act + kw).  Lanes l and l^32
+// hold the same sample.
+template <int T>
+__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& sc, float& us, float& ius) {
+  float m = 0.f;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
+  // seeded as bias / us stays finite)
+  const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
+  sc = __builtin_amdgcn_ldexpf(1.0f, 14 - e);
+  us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
+  ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
+}
+
+// Layer end: acc = acc * us + bias (f16x2: undo the scales) or acc + bias.
+template <int NT>
+__device__ __forceinline__ floatx16 x3_finish(const floatx16& acc, float us, const floatx16& b) {
+  if constexpr (NT == 2) {
+    floatx16 r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = __builtin_fmaf(acc[i], us, b[i]);
+    return r;
+  } else {
+    return acc + b;
+  }
+}
+
 // One weight group from LDS: input tile Q (2 k-steps of 16) into NOUT
-// output tiles.  Block (s, o, part) is 1 KiB at ((s*NOUT + o)*3 + part) KiB;
+// output tiles.  Block (s, o, part) is 1 KiB at ((s*NOUT + o)*NT + part) KiB;
 // lane l's 16 bytes at l*16.
-template <int T, int NOUT, int Q>
+template <int NT, int T, int NOUT, int Q>
 __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
-                                         int lane) {
+                                         int lane, float sc) {
+  using E = typename XT<NT>::E;
   const char* lb = buf + lane * 16;
 if constexpr (T == 8) {
   // A fragments one output tile ahead (LDS latency off the MFMA chain).
-  auto frag = [&](int t, bf16x8& ah, bf16x8& am, bf16x8& al) {
-    const char* a = lb + ((t * 3) << 10);
-    am = *reinterpret_cast<const bf16x8*>(a + 1024);
-    ah = *reinterpret_cast<const bf16x8*>(a);
-    al = *reinterpret_cast<const bf16x8*>(a + 2048);
-  };
-  bf16x8 ch, cm, cl;
-  frag(0, ch, cm, cl);
+  E c[NT];
+  load_frag<NT>(lb, c);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    bf16x8 bh, bm, bl;
-    if (s == 0) split8<0>(hb[Q], bh, bm, bl);
-    else split8<1>(hb[Q], bh, bm, bl);
+    E b[NT];
+    if (s == 0) splitk<NT, 0>(hb[Q], sc, b);
+    else splitk<NT, 1>(hb[Q], sc, b);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
       const int t = s * NOUT + o;
-      bf16x8 nh, nm, nl;
-      if (t + 1 < 2 * NOUT) frag(t + 1, nh, nm, nl);
-      acc[o] = mfma3(ch, cm, cl, bh, bm, bl, acc[o]);
+      E n[NT];
+      if (t + 1 < 2 * NOUT) load_frag<NT>(lb + (((t + 1) * NT) << 10), n);
+      acc[o] = mfma_split<NT>(c, b, acc[o]);
       if (t + 1 < 2 * NOUT) {
-        ch = nh;
-        cm = nm;
-        cl = nl;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) c[i] = n[i];
       }
     }
   }
 } else {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    bf16x8 bh, bm, bl;
-    if (s == 0) split8<0>(hb[Q], bh, bm, bl);
-    else split8<1>(hb[Q], bh, bm, bl);
+    E b[NT];
+    if (s == 0) splitk<NT, 0>(hb[Q], sc, b);
+    else splitk<NT, 1>(hb[Q], sc, b);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
-      const char* a = lb + (((s * NOUT + o) * 3) << 10);
-      const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
-      acc[o] = mfma3(ah, am, al, bh, bm, bl, acc[o]);
+      E a[NT];
+      load_frag<NT>(lb + (((s * NOUT + o) * NT) << 10), a);
+      acc[o] = mfma_split<NT>(a, b, acc[o]);
     }
   }
 }
@@ -174,23 +273,23 @@ struct X3Span {
   int next_pieces;      // KiB pieces of the next NSC's group 0
 };
 
-template <int T>
+template <int NT, int T>
 __device__ __forceinline__ int first_pieces(const DevOp& op) {
-  return (op.n_hidden > 1 ? group_bytes(T) : group_bytes(op.x3_tlast)) >> 10;
+  return (op.n_hidden > 1 ? group_bytes<NT>(T) : group_bytes<NT>(op.x3_tlast)) >> 10;
 }
 
-template <int T, bool INV>
+template <int NT, int T, bool INV>
 __device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int oi, int op_begin, int op_end) {
   const DevOp& op = F->ops[oi];
   X3Span sp;
   sp.base = op.x3;
   sp.G = op.x3_groups;
   sp.nhid = T * (op.n_hidden - 1);
-  sp.last_pieces = group_bytes(op.x3_tlast) >> 10;
+  sp.last_pieces = group_bytes<NT>(op.x3_tlast) >> 10;
   const int n = op.x3_next[INV ? 1 : 0];
   if (n >= op_begin && n < op_end) {
     sp.next_base = F->ops[n].x3;
-    sp.next_pieces = first_pieces<T>(F->ops[n]);
+    sp.next_pieces = first_pieces<NT, T>(F->ops[n]);
   } else {
     sp.next_base = -1;
     sp.next_pieces = 0;
@@ -218,9 +317,9 @@ struct X3Pipe {
 
 // DMA the group after group p.g (the next one of this NSC, or group 0 of
 // the next NSC) into `dst`; nothing at the end of the stream.
-template <int T>
+template <int NT, int T>
 __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
-  constexpr int kHid = group_bytes(T);
+  constexpr int kHid = group_bytes<NT>(T);
   const int g = p.g + 1;
   long long off;
   int pieces;
@@ -241,27 +340,28 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
 // One pipeline step: wait for this wave's DMAs, block barrier (the group in
 // buffer `buf` is complete and the other buffer is free), prefetch the next
 // group into it, then this group's MFMAs.  `bias` (optional): bias tiles of
-// a layer that started from zero, loaded here — in the layer's last step,
-// when its earlier input tiles are dead — and added after the MFMAs.
-template <int T, int NOUT, int Q, bool SW>
+// a layer whose accumulators did not start from the bias, loaded here — in
+// the layer's last step, when its earlier input tiles are dead — and joined
+// after the MFMAs (x3_finish, which also undoes the f16x2 scales).
+template <int NT, int T, int NOUT, int Q, bool SW>
 __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                        int hh) {
-  constexpr int kBuf = group_bytes(T);
+                                        int hh, float sc, float us) {
+  constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   X3_MARK(2);
-  x3_issue_next<T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
+  x3_issue_next<NT, T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   if (bias != nullptr) {
     floatx16 bt[NOUT];
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-    x3_group<T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane, sc);
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) acc[o] += bt[o];
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
   } else {
-    x3_group<T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
+    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane, sc);
   }
   // SW: the layer input arrives as pre-activations except tile 0; the swish
   // of tile Q+1 goes here, in the same scheduling region as this group's
@@ -273,12 +373,13 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   if constexpr (T == 8 && ZF_X3_WIDE_SCHED > 0) {
     // the k-step-0 split first, then every MFMA followed by its share of LDS
     // reads and VALU (split of k-step 1, the deferred swish)
-    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    constexpr int kP = XT<NT>::kProd;
+    __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
     __builtin_amdgcn_sched_group_barrier(0x402, 20, 0);
 #pragma unroll
-    for (int i = 0; i < 12 * NOUT; ++i) {
+    for (int i = 0; i < 2 * kP * NOUT; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if ((NT == 3 && i % 2 == 0) || (NT == 2 && i % 3 != 2)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_WIDE_SCHED, 0);
     }
   }
@@ -298,55 +399,52 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 #ifndef ZF_X3_PIPE_VALU
 #define ZF_X3_PIPE_VALU 0
 #endif
-template <int T, int NOUT, int Q, bool HASB>
+template <int NT, int T, int NOUT, int Q, bool HASB>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                             int hh, bf16x8 (&cs)[3]) {
-  constexpr int kBuf = group_bytes(T);
+                                             int hh, typename XT<NT>::E (&cs)[NT], float sc, float us) {
+  using E = typename XT<NT>::E;
+  constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   X3_MARK(2);
-  x3_issue_next<T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
+  x3_issue_next<NT, T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   floatx16 bt[NOUT];
   if constexpr (HASB) {
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
   }
   const char* lb = p.wbuf + p.buf * kBuf + lane * 16;
-  bf16x8 s1[3];
-  split8<1>(hb[Q], s1[0], s1[1], s1[2]);
+  E s1[NT];
+  splitk<NT, 1>(hb[Q], sc, s1);
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    const char* a = lb + ((o * 3) << 10);
-    const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
-    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
-    const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
-    acc[o] = mfma3(ah, am, al, cs[0], cs[1], cs[2], acc[o]);
+    E a[NT];
+    load_frag<NT>(lb + ((o * NT) << 10), a);
+    acc[o] = mfma_split<NT>(a, cs, acc[o]);
   }
   if constexpr (Q + 1 < T) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) hb[Q + 1][r] = swish(hb[Q + 1][r]);
-    split8<0>(hb[Q + 1], cs[0], cs[1], cs[2]);
+    splitk<NT, 0>(hb[Q + 1], sc, cs);
   }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
-    const char* a = lb + (((NOUT + o) * 3) << 10);
-    const bf16x8 am = *reinterpret_cast<const bf16x8*>(a + 1024);
-    const bf16x8 ah = *reinterpret_cast<const bf16x8*>(a);
-    const bf16x8 al = *reinterpret_cast<const bf16x8*>(a + 2048);
-    acc[o] = mfma3(ah, am, al, s1[0], s1[1], s1[2], acc[o]);
+    E a[NT];
+    load_frag<NT>(lb + (((NOUT + o) * NT) << 10), a);
+    acc[o] = mfma_split<NT>(a, s1, acc[o]);
   }
   if constexpr (HASB) {
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) acc[o] += bt[o];
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
   }
 #if ZF_X3_PIPE_VALU > 0
-  __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
 #pragma unroll
-  for (int i = 0; i < 12 * NOUT; ++i) {
+  for (int i = 0; i < 2 * XT<NT>::kProd * NOUT; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    if ((NT == 3 && i % 2 == 0) || (NT == 2 && i % 3 != 2)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_PIPE_VALU, 0);
   }
 #endif
@@ -355,28 +453,28 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 }
 
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
-template <int T, int NOUT, bool HASB, int Q = 0>
+template <int NT, int T, int NOUT, bool HASB, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                              bf16x8 (&cs)[3]) {
+                                              typename XT<NT>::E (&cs)[NT], float sc, float us) {
   if constexpr (Q + 1 < T) {
-    x3_step_pipe<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs);
-    x3_layer_pipe<T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs);
+    x3_step_pipe<NT, T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, sc, us);
+    x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, sc, us);
   } else {
-    x3_step_pipe<T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs);
+    x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, sc, us);
   }
 }
 
 // A whole streamed Dense layer: T groups (one per input tile).
-template <int T, int NOUT, bool SW, int Q = 0>
+template <int NT, int T, int NOUT, bool SW, int Q = 0>
 __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
-                                         floatx16 (&acc)[NOUT], int lane, const float* bias_last = nullptr,
-                                         int hh = 0) {
+                                         floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
+                                         float sc, float us) {
   if constexpr (Q + 1 < T) {
-    x3_step<T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh);
-    x3_layer<T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh);
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh, sc, us);
+    x3_layer<NT, T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, sc, us);
   } else {
-    x3_step<T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh);
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh, sc, us);
   }
 }
 
@@ -396,7 +494,7 @@ __device__ __forceinline__ float squareplus_rsq(float x) {
 // footprint is 2 groups + the state: 50 KiB at T = 4 (3 blocks = 3 waves per
 // SIMD, <= 168 VGPRs), 104 KiB at T = 8 (hidden 256: one block per CU, the
 // 8 + 8 accumulator tiles need one wave's whole register file).
-template <int K, int T, bool PAIRS, bool INV>
+template <int NT, int K, int T, bool PAIRS, bool INV>
 #ifndef ZF_X3_NARROW_OCC
 #define ZF_X3_NARROW_OCC 3
 #endif
@@ -415,7 +513,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
   const int lane = threadIdx.x & 63;
   const int s = lane & 31;
   const int hh = lane >> 5;
-  constexpr int kBuf = group_bytes(T);
+  constexpr int kBuf = group_bytes<NT>(T);
   // LDS: [2][kBuf] weight groups | [NW][D][32] state | [NW] partials
   float* xs = reinterpret_cast<float*>(lds + 2 * kBuf) + wave * (32 * D);
   double* s_part = reinterpret_cast<double*>(reinterpret_cast<float*>(lds + 2 * kBuf) + NW * 32 * D);
@@ -441,7 +539,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
       const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
       if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
     }
-    if (first >= 0) x3_dma(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<T>(F->ops[first]), wave, lane);
+    if (first >= 0) x3_dma(x3 + F->ops[first].x3, pipe.wbuf, first_pieces<NT, T>(F->ops[first]), wave, lane);
   }
 
   const KnotConsts kc(K);
@@ -455,7 +553,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
       shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
-      pipe.span = make_span<T, INV>(F, oi, op_begin, op_end);
+      pipe.span = make_span<NT, T, INV>(F, oi, op_begin, op_end);
       pipe.g = 0;
       floatx16 hb[T];
       X3_MARK(3);
@@ -469,16 +567,31 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
       X3_MARK(4);
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each; the biases
       // seed the accumulators.
+      // bf16x3: the biases seed the accumulators.  f16x2, hidden <= 128:
+      // they join at the layer's end with the unscale (x3_finish, one fma);
+      // hidden 256 (no registers to hold bias tiles there): they seed the
+      // accumulators divided by the unscale (exact: powers of two), and the
+      // accumulators are multiplied by it afterwards.
+      constexpr bool kSeedScaled = NT == 2 && T == 8;
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
+        float sc = 1.f, us = 1.f, ius = 1.f;
+        if constexpr (NT == 2) x3_act_scale<T>(hb, op.x3_kw[l], sc, us, ius);
 #pragma unroll
-        for (int o = 0; o < T; ++o) acc[o] = bias_acc(sp + op.b[l] + o * 32, hh);
+        for (int o = 0; o < T; ++o)
+          acc[o] = NT == 3 ? bias_acc(sp + op.b[l] + o * 32, hh)
+                           : (kSeedScaled ? bias_acc(sp + op.b[l] + o * 32, hh) * ius : floatx16{0});
+        const float* bh = (NT == 2 && !kSeedScaled) ? sp + op.b[l] : nullptr;
         if constexpr (kPipe) {
-          bf16x8 cs[3];
-          split8<0>(hb[0], cs[0], cs[1], cs[2]);
-          x3_layer_pipe<T, T, false>(x3, pipe, hb, acc, lane, nullptr, hh, cs);
+          typename XT<NT>::E cs[NT];
+          splitk<NT, 0>(hb[0], sc, cs);
+          x3_layer_pipe<NT, T, T, NT == 2>(x3, pipe, hb, acc, lane, bh, hh, cs, sc, us);
         } else {
-          x3_layer<T, T, true>(x3, pipe, hb, acc, lane);
+          x3_layer<NT, T, T, true>(x3, pipe, hb, acc, lane, bh, hh, sc, us);
+        }
+        if constexpr (kSeedScaled) {
+#pragma unroll
+          for (int o = 0; o < T; ++o) acc[o] *= us;
         }
         X3_MARK(5);
         const int nsw = (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
@@ -499,21 +612,30 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
       // PAIRS == false: one pair (dt <= 2), and the hidden activations are
       // dead once the last layer has consumed them.
       const int npair = PAIRS ? (dt + 1) / 2 : 1;
+      float lsc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
+      if constexpr (NT == 2) x3_act_scale<T>(hb, op.x3_kw[op.n_hidden], lsc, lus, lius);
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
         // live across pairs anyway; otherwise it joins in the last step, when
-        // the first input tiles are dead (fewer registers at the peak).
+        // the first input tiles are dead (fewer registers at the peak);
+        // f16x2 always joins it at the end, with the unscale.
         const float* bl = sp + op.x3_blast + pr * TL * 32;
         floatx16 pa[TL];
+        constexpr bool kSeed = PAIRS && NT == 3;
 #pragma unroll
-        for (int o = 0; o < TL; ++o) pa[o] = PAIRS ? bias_acc(bl + o * 32, hh) : floatx16{0};
+        for (int o = 0; o < TL; ++o)
+          pa[o] = kSeed ? bias_acc(bl + o * 32, hh) : (kSeedScaled ? bias_acc(bl + o * 32, hh) * lius : floatx16{0});
         X3_MARK(6);
         if constexpr (kPipe) {
-          bf16x8 cs[3];
-          split8<0>(hb[0], cs[0], cs[1], cs[2]);
-          x3_layer_pipe<T, TL, true>(x3, pipe, hb, pa, lane, bl, hh, cs);
+          typename XT<NT>::E cs[NT];
+          splitk<NT, 0>(hb[0], lsc, cs);
+          x3_layer_pipe<NT, T, TL, true>(x3, pipe, hb, pa, lane, bl, hh, cs, lsc, lus);
         } else {
-          x3_layer<T, TL, kLastSW>(x3, pipe, hb, pa, lane, PAIRS ? nullptr : bl, hh);
+          x3_layer<NT, T, TL, kLastSW>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh, lsc, lus);
+        }
+        if constexpr (kSeedScaled) {
+#pragma unroll
+          for (int o = 0; o < TL; ++o) pa[o] *= lus;
         }
         X3_MARK(7);
         float P[TL * 16];
@@ -617,6 +739,13 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   return true;
 }
 
+// Split scheme for new handles: ZF_X3_SCHEME=bf16x3 | f16x2 (default f16x2).
+int x3_scheme() {
+  const char* env = std::getenv("ZF_X3_SCHEME");
+  if (env && std::strcmp(env, "bf16x3") == 0) return 3;
+  return 2;
+}
+
 int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
 
 int x3_pairs(const zf_flow_desc& desc) { return (desc.dim / 2 + 1) / 2; }
@@ -624,7 +753,7 @@ int x3_pairs(const zf_flow_desc& desc) { return (desc.dim / 2 + 1) / 2; }
 // Pack the group streams (bf16 hi/mid/lo A fragments) of every NSC and the
 // row-permuted last-layer biases (into `packed` at F.ops[i].x3_blast, which
 // the caller allocated with x3_pairs * x3_last_tiles(K) * 32 floats).
-void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, float* packed,
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream) {
   stream.clear();
   int prev = -1;
@@ -649,11 +778,23 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, floa
       const int out = last ? dt * S : op.hidden[l];
       const int NOUT = last ? TL : T;
       const float* W = nat + op.off_w[l];
+      // f16x2: the layer's power-of-two scale, max |W| * 2^kw in [2^13, 2^14)
+      int kw = 0;
+      if (NT == 2) {
+        float mx = 0.f;
+        for (int64_t i = 0; i < (int64_t)in * out; ++i) mx = std::fmax(mx, std::fabs(W[i]));
+        if (mx > 0.f && std::isfinite(mx)) {
+          int e;
+          std::frexp(mx, &e);
+          kw = 14 - e;
+        }
+      }
+      d.x3_kw[l] = kw;
       for (int pr = 0; pr < (last ? NP : 1); ++pr)
         for (int q = 0; q < T; ++q)
           for (int s = 0; s < 2; ++s)
             for (int o = 0; o < NOUT; ++o) {
-              uint16_t part[3][64][8];
+              uint16_t part[3][64][8];  // [term][lane][element]
               for (int ln = 0; ln < 64; ++ln)
                 for (int j = 0; j < 8; ++j) {
                   const int kstep = 2 * q + s;
@@ -669,16 +810,24 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, floa
                     col = (dd < dt && jp < S) ? dd * S + jp : -1;
                   }
                   const float x = (k < in && col >= 0) ? W[(int64_t)k * out + col] : 0.f;
-                  const uint16_t bh = bf16_rne(x);
-                  const float r1 = x - bf16_f(bh);
-                  const uint16_t bm = bf16_rne(r1);
-                  const uint16_t bl = bf16_rne(r1 - bf16_f(bm));
-                  part[0][ln][j] = bh;
-                  part[1][ln][j] = bm;
-                  part[2][ln][j] = bl;
+                  if (NT == 3) {
+                    const uint16_t bh = bf16_rne(x);
+                    const float r1 = x - bf16_f(bh);
+                    const uint16_t bm = bf16_rne(r1);
+                    const uint16_t bl = bf16_rne(r1 - bf16_f(bm));
+                    part[0][ln][j] = bh;
+                    part[1][ln][j] = bm;
+                    part[2][ln][j] = bl;
+                  } else {
+                    const float xs = std::ldexp(x, kw);
+                    const _Float16 h = (_Float16)xs;  // RNE
+                    const _Float16 lo = (_Float16)(xs - (float)h);
+                    std::memcpy(&part[0][ln][j], &h, 2);
+                    std::memcpy(&part[1][ln][j], &lo, 2);
+                  }
                 }
               const uint16_t* pp = &part[0][0][0];
-              stream.insert(stream.end(), pp, pp + 3 * 64 * 8);
+              stream.insert(stream.end(), pp, pp + NT * 64 * 8);
             }
     }
     // permuted last bias: [pair][o][lane half h][r] = bias[(2 pair + h) S + 16o + r]
@@ -693,23 +842,23 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, DevFlow& F, floa
   }
 }
 
-size_t x3_lds_bytes(int T, int D) {
-  return (size_t)2 * group_bytes(T) + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
+size_t x3_lds_bytes(int T, int D, int NT) {
+  return (size_t)2 * 2 * T * NT * 1024 + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
 }
 
-template <int K, int T, bool PAIRS>
+template <int NT, int K, int T, bool PAIRS>
 int launch_x3(const X3Launch& a, bool inverse) {
   const long long rows = kX3Waves * kTile;
   const long long grid = (a.N + rows - 1) / rows;
   if (grid > 0x7fffffffLL) return einval("N too large");
-  const size_t lds = x3_lds_bytes(T, a.D);
+  const size_t lds = x3_lds_bytes(T, a.D, NT);
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
-    hipLaunchKernelGGL((flow_kernel_x3<K, T, PAIRS, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
-    hipLaunchKernelGGL((flow_kernel_x3<K, T, PAIRS, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
@@ -718,12 +867,19 @@ int launch_x3(const X3Launch& a, bool inverse) {
 
 // Instantiated shapes (x3_eligible): hidden <= 128 with K 8/16 and dt <= 2
 // (cfg1-4, deep-set); hidden <= 256 with K 16/32, any dt <= 8 (cfg5).
+template <int NT>
+int launch_x3_nt(const X3Launch& a, bool inverse) {
+  if (a.T == 4 && a.K == 8) return launch_x3<NT, 8, 4, false>(a, inverse);
+  if (a.T == 4 && a.K == 16) return launch_x3<NT, 16, 4, false>(a, inverse);
+  if (a.T == 8 && a.K == 16) return launch_x3<NT, 16, 8, true>(a, inverse);
+  if (a.T == 8 && a.K == 32) return launch_x3<NT, 32, 8, true>(a, inverse);
+  return enotsup("split-MFMA kernel: shape not instantiated");
+}
+
 int launch_flow_x3(const X3Launch& a, bool inverse) {
-  if (a.T == 4 && a.K == 8) return launch_x3<8, 4, false>(a, inverse);
-  if (a.T == 4 && a.K == 16) return launch_x3<16, 4, false>(a, inverse);
-  if (a.T == 8 && a.K == 16) return launch_x3<16, 8, true>(a, inverse);
-  if (a.T == 8 && a.K == 32) return launch_x3<32, 8, true>(a, inverse);
-  return enotsup("bf16x3 kernel: shape not instantiated");
+  if (a.NT == 2) return launch_x3_nt<2>(a, inverse);
+  if (a.NT == 3) return launch_x3_nt<3>(a, inverse);
+  return einval("split-MFMA kernel: scheme %d", a.NT);
 }
 
 #if ZF_X3_TRACE
