@@ -48,16 +48,17 @@ def _fingerprint() -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    """Compile every HIP source into one shared library (skip if up to date)."""
-    stamp = HERE / ".libzenflow_amd.sha256"
-    fp = _fingerprint()
-    if not force and LIB.exists() and stamp.exists() and stamp.read_text() == fp:
-        return LIB
-    tmp = LIB.with_suffix(".so.tmp")
-    objdir = HERE.parent / "build" / "obj"
+def build(force: bool = False, verbose: bool = True, out: Path = LIB, extra=()) -> Path:
+    """Compile every HIP source into one shared library (skip if up to date).
+    ``out``/``extra``: tuning builds (e.g. ``-DZF_X3_TRACE=1``) into another file."""
+    stamp = out.parent / f".{out.stem}.sha256"
+    fp = _fingerprint() + " ".join(extra)
+    if not force and out.exists() and stamp.exists() and stamp.read_text() == fp:
+        return out
+    tmp = out.with_suffix(".so.tmp")
+    objdir = HERE.parent / "build" / ("obj" if not extra else "obj_" + hashlib.sha1(" ".join(extra).encode()).hexdigest()[:8])
     objdir.mkdir(parents=True, exist_ok=True)
-    compile_flags = [f for f in FLAGS if f != "-shared"]
+    compile_flags = [f for f in FLAGS if f != "-shared"] + list(extra)
 
     def _compile(src: str) -> Path:
         obj = objdir / (Path(src).stem + ".o")
@@ -75,10 +76,17 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     if verbose:
         print("[zenflow_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     stamp.write_text(fp)
-    return LIB
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python -m zenflow_amd.build [--force] [--out PATH] [-DMACRO=V ...]
+    argv = sys.argv[1:]
+    o = LIB
+    if "--out" in argv:
+        i = argv.index("--out")
+        o = Path(argv[i + 1]).resolve()
+        del argv[i : i + 2]
+    build(force="--force" in argv, out=o, extra=[a for a in argv if a.startswith("-D")])

@@ -126,7 +126,7 @@ __device__ __forceinline__ void spline_pair(float* ring, float* xs, int s, int h
     p.sy = sy;
     p.rsx = rcp_refined(sx);
     p.rsy = rcp_refined(sy);
-    float* xp = xs + pmod(d + rot, D) * 32 + s;
+    float* xp = xs + wrap(d + rot, D) * 32 + s;
     const float xv = *xp;
     const RqsBin bin = rqs_bin<!INV>(xv, K, p);
     if (!INV) {

@@ -133,6 +133,10 @@ __device__ __forceinline__ int pmod(int a, int m) {
   return r < 0 ? r + m : r;
 }
 
+// a mod m for a in [0, 2m): stored-column index of logical dim j under a
+// rotation rot in [0, m) (no integer division on the per-sample path).
+__device__ __forceinline__ int wrap(int a, int m) { return a >= m ? a - m : a; }
+
 // softmax_with_threshold constants (utils.py:32-34): c and 1 + c*n are Python
 // floats (fp64), rounded to fp32 where they meet fp32 arrays.
 struct KnotConsts {
@@ -165,7 +169,7 @@ __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, fl
   if (!INV) {
     float ldsb = 0.f;
     for (int i = 0; i < D; ++i) {
-      const int p = pmod(i + rot, D);
+      const int p = wrap(i + rot, D);
       const float v = xs[p * 32 + s];
       const int mode = (int)sb[8 * i];
       const float a = sb[8 * i + 1], b = sb[8 * i + 2], xmin = sb[8 * i + 3];
@@ -188,7 +192,7 @@ __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, fl
     ld = ld + ldsb;
   } else {
     for (int i = 0; i < D; ++i) {
-      const int p = pmod(i + rot, D);
+      const int p = wrap(i + rot, D);
       const float zv = xs[p * 32 + s];
       const int mode = (int)sb[8 * i];
       const float a = sb[8 * i + 1], b = sb[8 * i + 2];
@@ -222,7 +226,7 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
   for (int ks = 0; ks < KS0; ++ks) {
     const int k = 2 * ks + hh;
     float v = 0.f;
-    if (k < dc) v = xs[pmod(dt + k + rot, D) * 32 + s];
+    if (k < dc) v = xs[wrap(dt + k + rot, D) * 32 + s];
     else if (k < DC) v = valid ? cin[row * C + (k - dc)] : 0.f;
     const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
     const float* w0 = blob + op.w[0] + ks * 64 + lane;
@@ -256,7 +260,7 @@ __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, con
     const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
     float lat = 0.f;
     for (int j = 0; j < D; ++j) {
-      const float v = xs[pmod(j + rot, D) * 32 + s];
+      const float v = xs[wrap(j + rot, D) * 32 + s];
       float t;
       if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
         // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
@@ -301,7 +305,7 @@ __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, con
     }
   }
   if (y_out != nullptr && valid) {
-    for (int j = hh; j < D; j += 2) y_out[row * D + j] = xs[pmod(j + rot, D) * 32 + s];
+    for (int j = hh; j < D; j += 2) y_out[row * D + j] = xs[wrap(j + rot, D) * 32 + s];
   }
   if (ld_out != nullptr && valid && hh == 0) ld_out[row] = ld;
 }

@@ -75,6 +75,12 @@ struct XT<2> {
 #define ZF_X3_WIDE_SCHED 3
 #endif
 
+// f16x2, hidden <= 128: seed the accumulators with bias / us (1) instead of
+// joining the bias at the layer's end with one fma (0).
+#ifndef ZF_X3_SEED_SCALED
+#define ZF_X3_SEED_SCALED 1
+#endif
+
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
 template <int NT>
@@ -122,13 +128,13 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
   }
 }
 
-// Regs 8s..8s+7 of an accumulator tile, scaled by sc (a power of two) -> hi /
-// lo fp16x8 (RNE each; the residual x*sc - hi is exact).
+// Regs 8s..8s+7 of an (already scaled) activation tile -> hi / lo fp16x8
+// (RNE each; the residual x - hi is exact).
 template <int S>
-__device__ __forceinline__ void split8h(const floatx16& v, float sc, halfx8& bh, halfx8& bl) {
+__device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& bl) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]} * sc;
+    const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
     const halfx2 h = __builtin_convertvector(x, halfx2);
     const floatx2 r = x - __builtin_convertvector(h, floatx2);
     const halfx2 l = __builtin_convertvector(r, halfx2);
@@ -138,12 +144,28 @@ __device__ __forceinline__ void split8h(const floatx16& v, float sc, halfx8& bh,
 }
 
 template <int NT, int S>
-__device__ __forceinline__ void splitk(const floatx16& v, float sc, typename XT<NT>::E (&b)[NT]) {
+__device__ __forceinline__ void splitk(const floatx16& v, typename XT<NT>::E (&b)[NT]) {
   if constexpr (NT == 3) {
     split8<S>(v, b[0], b[1], b[2]);
   } else {
-    split8h<S>(v, sc, b[0], b[1]);
+    split8h<S>(v, b[0], b[1]);
   }
+}
+
+// Layer-input activation: swish(v) (bf16x3), or f16x2's swish(v) * sc with
+// isc = 1/sc a power of two folded into the reciprocal — rcp((1+e)*isc) =
+// sc*rcp(1+e) exactly — so the scale costs no instruction (swish mode 0).
+template <int NT>
+__device__ __forceinline__ float act_swish(float v, float isc) {
+#if ZF_SWISH_MODE == 0
+  if constexpr (NT == 2) {
+    const float e = __builtin_amdgcn_exp2f(-v * 1.44269504f);
+    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(e, isc, isc));
+  }
+  return swish(v);
+#else
+  return NT == 2 ? swish(v) / isc : swish(v);
+#endif
 }
 
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
@@ -180,13 +202,13 @@ __device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)
   else f[1] = *reinterpret_cast<const E*>(a + 1024);
 }
 
-// f16x2: per-sample power-of-two scale of a layer input so its largest
-// |value| lands in [2^13, 2^14) (|swish(v)| <= |v|, so raw pre-activations
-// of deferred tiles bound their swish), and the exact factor that undoes
-// both scales on the accumulator: us = 2^-(e_act + kw).  Lanes l and l^32
+// f16x2: per-sample power-of-two scale sc = 1/isc of a layer input, from its
+// raw pre-activations, so its largest |swish| lands below 2^14 (|swish(v)| <=
+// |v|), and the exact factor that undoes both scales on the accumulator:
+// us = 2^-(e_act + kw) (ius = 1/us).  Lanes l and l^32
 // hold the same sample.
 template <int T>
-__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& sc, float& us, float& ius) {
+__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius) {
   float m = 0.f;
 #pragma unroll
   for (int t = 0; t < T; ++t)
@@ -196,7 +218,7 @@ __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, fl
   // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
   // seeded as bias / us stays finite)
   const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
-  sc = __builtin_amdgcn_ldexpf(1.0f, 14 - e);
+  isc = __builtin_amdgcn_ldexpf(1.0f, e - 14);
   us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
   ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
 }
@@ -219,7 +241,7 @@ __device__ __forceinline__ floatx16 x3_finish(const floatx16& acc, float us, con
 // lane l's 16 bytes at l*16.
 template <int NT, int T, int NOUT, int Q>
 __device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
-                                         int lane, float sc) {
+                                         int lane) {
   using E = typename XT<NT>::E;
   const char* lb = buf + lane * 16;
 if constexpr (T == 8) {
@@ -229,8 +251,8 @@ if constexpr (T == 8) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     E b[NT];
-    if (s == 0) splitk<NT, 0>(hb[Q], sc, b);
-    else splitk<NT, 1>(hb[Q], sc, b);
+    if (s == 0) splitk<NT, 0>(hb[Q], b);
+    else splitk<NT, 1>(hb[Q], b);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
       const int t = s * NOUT + o;
@@ -247,8 +269,8 @@ if constexpr (T == 8) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     E b[NT];
-    if (s == 0) splitk<NT, 0>(hb[Q], sc, b);
-    else splitk<NT, 1>(hb[Q], sc, b);
+    if (s == 0) splitk<NT, 0>(hb[Q], b);
+    else splitk<NT, 1>(hb[Q], b);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) {
       E a[NT];
@@ -346,7 +368,7 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
 template <int NT, int T, int NOUT, int Q, bool SW>
 __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                        int hh, float sc, float us) {
+                                        int hh, float isc, float us) {
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -357,18 +379,18 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
     floatx16 bt[NOUT];
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane, sc);
+    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
   } else {
-    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane, sc);
+    x3_group<NT, T, NOUT, Q>(p.wbuf + p.buf * kBuf, hb, acc, lane);
   }
   // SW: the layer input arrives as pre-activations except tile 0; the swish
   // of tile Q+1 goes here, in the same scheduling region as this group's
   // MFMAs, whose issue gaps it fills.
   if constexpr (SW && Q + 1 < T) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = swish(hb[Q + 1][r]);
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
   }
   if constexpr (T == 8 && ZF_X3_WIDE_SCHED > 0) {
     // the k-step-0 split first, then every MFMA followed by its share of LDS
@@ -402,7 +424,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 template <int NT, int T, int NOUT, int Q, bool HASB>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                             int hh, typename XT<NT>::E (&cs)[NT], float sc, float us) {
+                                             int hh, typename XT<NT>::E (&cs)[NT], float isc, float us) {
   using E = typename XT<NT>::E;
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
@@ -417,7 +439,7 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   }
   const char* lb = p.wbuf + p.buf * kBuf + lane * 16;
   E s1[NT];
-  splitk<NT, 1>(hb[Q], sc, s1);
+  splitk<NT, 1>(hb[Q], s1);
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
     E a[NT];
@@ -426,8 +448,8 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   }
   if constexpr (Q + 1 < T) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = swish(hb[Q + 1][r]);
-    splitk<NT, 0>(hb[Q + 1], sc, cs);
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+    splitk<NT, 0>(hb[Q + 1], cs);
   }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
@@ -456,12 +478,12 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 template <int NT, int T, int NOUT, bool HASB, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                              typename XT<NT>::E (&cs)[NT], float sc, float us) {
+                                              typename XT<NT>::E (&cs)[NT], float isc, float us) {
   if constexpr (Q + 1 < T) {
-    x3_step_pipe<NT, T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, sc, us);
-    x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, sc, us);
+    x3_step_pipe<NT, T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us);
+    x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
   } else {
-    x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, sc, us);
+    x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
   }
 }
 
@@ -469,12 +491,12 @@ __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pip
 template <int NT, int T, int NOUT, bool SW, int Q = 0>
 __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                          floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                         float sc, float us) {
+                                         float isc, float us) {
   if constexpr (Q + 1 < T) {
-    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh, sc, us);
-    x3_layer<NT, T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, sc, us);
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh, isc, us);
+    x3_layer<NT, T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
   } else {
-    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh, sc, us);
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
   }
 }
 
@@ -562,21 +584,26 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
       // which passes over its input once per dim pair.
       constexpr bool kLastSW = !PAIRS;
       constexpr bool kPipe = T == 4 && !PAIRS && ZF_X3_PIPE;
+      // f16x2: every layer leaves raw pre-activations; the next streamed
+      // layer scales and swishes them (act_swish) as it goes.
       layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
-                (op.n_hidden > 1 || kLastSW) ? 1 : T);
+                NT == 2 ? 0 : (op.n_hidden > 1 || kLastSW) ? 1 : T);
       X3_MARK(4);
-      // Hidden layers 1..n_hidden-1 (:343-345), T groups each; the biases
-      // seed the accumulators.
-      // bf16x3: the biases seed the accumulators.  f16x2, hidden <= 128:
-      // they join at the layer's end with the unscale (x3_finish, one fma);
-      // hidden 256 (no registers to hold bias tiles there): they seed the
-      // accumulators divided by the unscale (exact: powers of two), and the
-      // accumulators are multiplied by it afterwards.
-      constexpr bool kSeedScaled = NT == 2 && T == 8;
+      // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
+      // biases seed the accumulators.  f16x2: they seed them divided by the
+      // unscale (exact: powers of two) and the accumulators are multiplied
+      // by it afterwards (kSeedScaled), or — ZF_X3_SEED_SCALED=0, hidden
+      // <= 128 — they join at the layer's end with the unscale in one fma
+      // (x3_finish; bias tiles live beside the accumulators there).
+      constexpr bool kSeedScaled = NT == 2 && (T == 8 || ZF_X3_SEED_SCALED);
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
-        float sc = 1.f, us = 1.f, ius = 1.f;
-        if constexpr (NT == 2) x3_act_scale<T>(hb, op.x3_kw[l], sc, us, ius);
+        float isc = 1.f, us = 1.f, ius = 1.f;
+        if constexpr (NT == 2) {
+          x3_act_scale<T>(hb, op.x3_kw[l], isc, us, ius);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hb[0][r] = act_swish<NT>(hb[0][r], isc);
+        }
 #pragma unroll
         for (int o = 0; o < T; ++o)
           acc[o] = NT == 3 ? bias_acc(sp + op.b[l] + o * 32, hh)
@@ -584,17 +611,17 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
         const float* bh = (NT == 2 && !kSeedScaled) ? sp + op.b[l] : nullptr;
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
-          splitk<NT, 0>(hb[0], sc, cs);
-          x3_layer_pipe<NT, T, T, NT == 2>(x3, pipe, hb, acc, lane, bh, hh, cs, sc, us);
+          splitk<NT, 0>(hb[0], cs);
+          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us);
         } else {
-          x3_layer<NT, T, T, true>(x3, pipe, hb, acc, lane, bh, hh, sc, us);
+          x3_layer<NT, T, T, true>(x3, pipe, hb, acc, lane, bh, hh, isc, us);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
           for (int o = 0; o < T; ++o) acc[o] *= us;
         }
         X3_MARK(5);
-        const int nsw = (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
+        const int nsw = NT == 2 ? 0 : (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
 #pragma unroll
         for (int o = 0; o < T; ++o) {
           if (o < nsw) {
@@ -612,8 +639,16 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
       // PAIRS == false: one pair (dt <= 2), and the hidden activations are
       // dead once the last layer has consumed them.
       const int npair = PAIRS ? (dt + 1) / 2 : 1;
-      float lsc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
-      if constexpr (NT == 2) x3_act_scale<T>(hb, op.x3_kw[op.n_hidden], lsc, lus, lius);
+      float lisc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
+      if constexpr (NT == 2) {
+        x3_act_scale<T>(hb, op.x3_kw[op.n_hidden], lisc, lus, lius);
+        // PAIRS: the input is read once per dim pair, so swish it whole here
+#pragma unroll
+        for (int o = 0; o < T; ++o)
+          if (o == 0 || !kLastSW)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hb[o][r] = act_swish<NT>(hb[o][r], lisc);
+      }
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
         // live across pairs anyway; otherwise it joins in the last step, when
@@ -628,10 +663,10 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
         X3_MARK(6);
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
-          splitk<NT, 0>(hb[0], lsc, cs);
-          x3_layer_pipe<NT, T, TL, true>(x3, pipe, hb, pa, lane, bl, hh, cs, lsc, lus);
+          splitk<NT, 0>(hb[0], cs);
+          x3_layer_pipe<NT, T, TL, !kSeedScaled>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus);
         } else {
-          x3_layer<NT, T, TL, kLastSW>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh, lsc, lus);
+          x3_layer<NT, T, TL, kLastSW>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh, lisc, lus);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
@@ -670,7 +705,7 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
           float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
           for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
-          float* xp = xs + pmod((act ? d : 0) + rot, D) * 32 + s;
+          float* xp = xs + wrap((act ? d : 0) + rot, D) * 32 + s;
           const float xv = *xp;
           const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
                                                        [](float v) { return v == 0.f ? 1.f : squareplus_rsq(v); });
