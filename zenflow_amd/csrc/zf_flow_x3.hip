@@ -81,6 +81,12 @@ struct XT<2> {
 #define ZF_X3_SEED_SCALED 1
 #endif
 
+// Timing-only ablations for tuning builds (results are wrong): 1 no spline
+// math, 2 no block barrier, 3 no MFMA, 4 no swish.
+#ifndef ZF_X3_ABLATE
+#define ZF_X3_ABLATE 0
+#endif
+
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
 template <int NT>
@@ -129,9 +135,28 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
 }
 
 // Regs 8s..8s+7 of an (already scaled) activation tile -> hi / lo fp16x8
-// (RNE each; the residual x - hi is exact).
+// (RNE each; the residual x - hi is exact).  ZF_X3_MIXSPLIT: the lo term by
+// v_fma_mix{lo,hi}_f16 (x*1 - f32(hi) rounded to f16 in one instruction:
+// 3 instead of 5 VALU per value pair, bit-identical —
+// tests/hip/f16_split_mix.hip).
+#ifndef ZF_X3_MIXSPLIT
+#define ZF_X3_MIXSPLIT 1
+#endif
 template <int S>
 __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& bl) {
+#if ZF_X3_MIXSPLIT
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = v[8 * S + 2 * i], x1 = v[8 * S + 2 * i + 1];
+    const halfx2 hv = __builtin_convertvector(floatx2{x0, x1}, halfx2);
+    __builtin_memcpy(&h[i], &hv, 4);
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(l[i]) : "v"(x0), "v"(h[i]));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l[i]) : "v"(x1), "v"(h[i]));
+  }
+  __builtin_memcpy(&bh, h, 16);
+  __builtin_memcpy(&bl, l, 16);
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
@@ -141,6 +166,7 @@ __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& b
     bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
     bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
   }
+#endif
 }
 
 template <int NT, int S>
@@ -157,6 +183,9 @@ __device__ __forceinline__ void splitk(const floatx16& v, typename XT<NT>::E (&b
 // sc*rcp(1+e) exactly — so the scale costs no instruction (swish mode 0).
 template <int NT>
 __device__ __forceinline__ float act_swish(float v, float isc) {
+#if ZF_X3_ABLATE == 4
+  return v;
+#endif
 #if ZF_SWISH_MODE == 0
   if constexpr (NT == 2) {
     const float e = __builtin_amdgcn_exp2f(-v * 1.44269504f);
@@ -183,6 +212,10 @@ __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, co
 template <int NT>
 __device__ __forceinline__ floatx16 mfma_split(const typename XT<NT>::E (&a)[NT], const typename XT<NT>::E (&b)[NT],
                                                floatx16 acc) {
+#if ZF_X3_ABLATE == 3
+  acc[0] += (float)a[0][0] * (float)b[0][0];
+  return acc;
+#endif
   if constexpr (NT == 3) {
     return mfma3(a[0], a[1], a[2], b[0], b[1], b[2], acc);
   } else {
@@ -372,7 +405,9 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if ZF_X3_ABLATE != 2
   __syncthreads();
+#endif
   X3_MARK(2);
   x3_issue_next<NT, T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   if (bias != nullptr) {
@@ -429,7 +464,9 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if ZF_X3_ABLATE != 2
   __syncthreads();
+#endif
   X3_MARK(2);
   x3_issue_next<NT, T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   floatx16 bt[NOUT];
@@ -508,6 +545,45 @@ __device__ __forceinline__ float squareplus_rsq(float x) {
   float sq = a * r;
   sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * r, sq);
   return 0.5f * (x + sq);
+}
+
+// Spline arithmetic of the split-MFMA kernel (ZF_X3_FASTSPLINE=1): the
+// spline parameters already differ from the reference's in the last ulp
+// (GEMM summation order), so the per-lane spline uses ~1-ulp hardware forms:
+// squareplus from v_sqrt_f32 (no Newton step), quotients from a refined
+// reciprocal, and the log-det as ONE log of the product of its three terms
+// (2 log(sk+eps) + log(num2+eps) - 2 log(den+eps), utils.py:133-135).
+// Parity is checked by the same per-sample tolerance as every other path.
+#ifndef ZF_X3_FASTSPLINE
+#define ZF_X3_FASTSPLINE 1
+#endif
+__device__ __forceinline__ float x3_squareplus(float x) {
+#if ZF_X3_FASTSPLINE
+  return 0.5f * (x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f)));
+#else
+  return squareplus_rsq(x);
+#endif
+}
+
+__device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
+#if ZF_X3_FASTSPLINE
+  const float rw = rcp_refined(b.w);
+  const float sk = b.h * rw;
+  const float zr = (x - b.xk) * rw;  // :122
+  const float z = (zr != zr) ? zr : fminf(fmaxf(zr, kEps), kOneMinusEps);
+  const float az = 1.0f - z;
+  const float num = b.h * z * (sk * z + b.dk * az);                // :125
+  const float den = sk + (b.dkp1 + b.dk - 2.0f * sk) * z * az;     // :126
+  const float rd = rcp_refined(den + kEps);
+  const float yv = b.yk + num * rd;                                // :127
+  y = b.oob ? x : yv;                                              // :130
+  const float num2 = z * (b.dkp1 * z + 2.0f * sk * az) + b.dk * (az * az);  // :133
+  const float sq = (sk + kEps) * rd;
+  const float l = __logf((num2 + kEps) * (sq * sq));
+  ld = b.oob ? 0.0f : l;                                           // :138
+#else
+  rqs_forward_eval(x, b, y, ld);
+#endif
 }
 
 // Block: 4 waves x 32 samples, one 32-row input tile per weight group,
@@ -687,8 +763,8 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
           float sx = 0.f, sy = 0.f;
 #pragma unroll
           for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-            w[j] = squareplus_rsq(P[j]);
-            hg[j] = squareplus_rsq(P[K + j]);
+            w[j] = x3_squareplus(P[j]);
+            hg[j] = x3_squareplus(P[K + j]);
             sx = sx + w[j];
             sy = sy + hg[j];
           }
@@ -708,15 +784,20 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
           float* xp = xs + wrap((act ? d : 0) + rot, D) * 32 + s;
           const float xv = *xp;
           const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
-                                                       [](float v) { return v == 0.f ? 1.f : squareplus_rsq(v); });
+                                                       [](float v) { return v == 0.f ? 1.f : x3_squareplus(v); });
           float yv;
+#if ZF_X3_ABLATE == 1
+          yv = xv + P[0] + P[TL * 16 - 1];
+          ldv = P[1];
+#else
           if (!INV) {
             float l;
-            rqs_forward_eval(xv, bin, yv, l);
+            x3_forward_eval(xv, bin, yv, l);
             ldv = act ? l : 0.f;
           } else {
             yv = rqs_inverse_eval(xv, bin);
           }
+#endif
           if (act) *xp = yv;
         }
         wave_lds_sync();
