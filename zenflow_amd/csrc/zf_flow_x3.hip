@@ -145,15 +145,30 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
 template <int S>
 __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& bl) {
 #if ZF_X3_MIXSPLIT
+  // One asm statement for all eight lo terms, ending in `s_nop 1`: hipcc
+  // pads no hazard inside or after an asm statement, and its outputs feed an
+  // MFMA operand, which needs two wait states after a VALU write (without
+  // the pad a schedule that put the MFMA right behind the asm read stale
+  // operands).
   uint32_t h[4], l[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float x0 = v[8 * S + 2 * i], x1 = v[8 * S + 2 * i + 1];
-    const halfx2 hv = __builtin_convertvector(floatx2{x0, x1}, halfx2);
+    const halfx2 hv = __builtin_convertvector(floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]}, halfx2);
     __builtin_memcpy(&h[i], &hv, 4);
-    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(l[i]) : "v"(x0), "v"(h[i]));
-    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l[i]) : "v"(x1), "v"(h[i]));
   }
+  asm(
+      "v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, 1.0, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, 1.0, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, 1.0, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, 1.0, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(l[0]), "=&v"(l[1]), "=&v"(l[2]), "=&v"(l[3])
+      : "v"(v[8 * S + 0]), "v"(v[8 * S + 1]), "v"(v[8 * S + 2]), "v"(v[8 * S + 3]), "v"(v[8 * S + 4]),
+        "v"(v[8 * S + 5]), "v"(v[8 * S + 6]), "v"(v[8 * S + 7]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
   __builtin_memcpy(&bh, h, 16);
   __builtin_memcpy(&bl, l, 16);
 #else
@@ -178,22 +193,29 @@ __device__ __forceinline__ void splitk(const floatx16& v, typename XT<NT>::E (&b
   }
 }
 
-// Layer-input activation: swish(v) (bf16x3), or f16x2's swish(v) * sc with
-// isc = 1/sc a power of two folded into the reciprocal — rcp((1+e)*isc) =
-// sc*rcp(1+e) exactly — so the scale costs no instruction (swish mode 0).
+// f16x2: every swished layer (Dense_0 .. Dense_{n_hidden-1}) is packed with
+// its weights and bias multiplied by log2(e) (x3_pack), so its accumulator
+// holds v' = v*log2(e) and the sigmoid's exponent needs no multiply.
+constexpr float kSwishPrescale = 1.44269504088896341f;
+
+// Layer-input activation: swish(v) (bf16x3), or f16x2's swish(v) * sc from
+// the prescaled v' with c = isc*log2(e) (isc = 1/sc a power of two):
+//   swish(v) * sc = v' / ((1 + 2^-v') * c)  — one fma, exp2, rcp, mul, so
+// neither the exponent scale nor the activation scale costs an instruction.
 template <int NT>
-__device__ __forceinline__ float act_swish(float v, float isc) {
+__device__ __forceinline__ float act_swish(float v, float c) {
 #if ZF_X3_ABLATE == 4
   return v;
 #endif
 #if ZF_SWISH_MODE == 0
   if constexpr (NT == 2) {
-    const float e = __builtin_amdgcn_exp2f(-v * 1.44269504f);
-    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(e, isc, isc));
+    const float e = __builtin_amdgcn_exp2f(-v);
+    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(e, c, c));
   }
   return swish(v);
 #else
-  return NT == 2 ? swish(v) / isc : swish(v);
+  if constexpr (NT == 2) return swish(v * (1.0f / kSwishPrescale)) * (kSwishPrescale / c);
+  return swish(v);
 #endif
 }
 
@@ -236,9 +258,10 @@ __device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)
 }
 
 // f16x2: per-sample power-of-two scale sc = 1/isc of a layer input, from its
-// raw pre-activations, so its largest |swish| lands below 2^14 (|swish(v)| <=
-// |v|), and the exact factor that undoes both scales on the accumulator:
-// us = 2^-(e_act + kw) (ius = 1/us).  Lanes l and l^32
+// raw (log2(e)-prescaled) pre-activations, so its largest |swish| lands below
+// 2^14 (|swish(v)| <= |v| < |v'|), and the exact factor that undoes both
+// scales on the accumulator: us = 2^-(e_act + kw) (ius = 1/us).  Returned
+// in isc: the swish constant c = isc*log2(e) (act_swish).  Lanes l and l^32
 // hold the same sample.
 template <int T>
 __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius) {
@@ -251,7 +274,7 @@ __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, fl
   // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
   // seeded as bias / us stays finite)
   const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
-  isc = __builtin_amdgcn_ldexpf(1.0f, e - 14);
+  isc = __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
   us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
   ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
 }
@@ -565,6 +588,16 @@ __device__ __forceinline__ float x3_squareplus(float x) {
 #endif
 }
 
+// 2*squareplus(x): the widths and heights are normalised by their sum, so the
+// factor 1/2 cancels exactly (a power of two): bit-identical knots.
+__device__ __forceinline__ float x3_squareplus2(float x) {
+#if ZF_X3_FASTSPLINE
+  return x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f));
+#else
+  return 2.0f * squareplus_rsq(x);
+#endif
+}
+
 __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
 #if ZF_X3_FASTSPLINE
   const float rw = rcp_refined(b.w);
@@ -763,12 +796,13 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
           float sx = 0.f, sy = 0.f;
 #pragma unroll
           for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-            w[j] = x3_squareplus(P[j]);
-            hg[j] = x3_squareplus(P[K + j]);
+            w[j] = x3_squareplus2(P[j]);
+            hg[j] = x3_squareplus2(P[K + j]);
             sx = sx + w[j];
             sy = sy + hg[j];
           }
-          // (v / sum + c) / (1 + c K) as one fma per knot: the parameters
+          // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
+          // 2*squareplus: the same quotient bits): the parameters
           // themselves already differ from the reference's in the last ulp
           // (GEMM summation order), so correctly rounded divisions buy nothing.
           const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
@@ -898,7 +932,8 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
       int kw = 0;
       if (NT == 2) {
         float mx = 0.f;
-        for (int64_t i = 0; i < (int64_t)in * out; ++i) mx = std::fmax(mx, std::fabs(W[i]));
+        for (int64_t i = 0; i < (int64_t)in * out; ++i)
+          mx = std::fmax(mx, std::fabs(W[i] * (last ? 1.0f : kSwishPrescale)));
         if (mx > 0.f && std::isfinite(mx)) {
           int e;
           std::frexp(mx, &e);
@@ -906,6 +941,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
         }
       }
       d.x3_kw[l] = kw;
+      const float pre = (NT == 2 && !last) ? kSwishPrescale : 1.0f;
       for (int pr = 0; pr < (last ? NP : 1); ++pr)
         for (int q = 0; q < T; ++q)
           for (int s = 0; s < 2; ++s)
@@ -935,7 +971,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
                     part[1][ln][j] = bm;
                     part[2][ln][j] = bl;
                   } else {
-                    const float xs = std::ldexp(x, kw);
+                    const float xs = std::ldexp(x * pre, kw);
                     const _Float16 h = (_Float16)xs;  // RNE
                     const _Float16 lo = (_Float16)(xs - (float)h);
                     std::memcpy(&part[0][ln][j], &h, 2);
@@ -945,6 +981,14 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
               const uint16_t* pp = &part[0][0][0];
               stream.insert(stream.end(), pp, pp + NT * 64 * 8);
             }
+    }
+    // f16x2: Dense_0 (fp32 fragments, d.w[0]) and the hidden biases of the
+    // swished layers join the log2(e) prescale (act_swish).
+    if (NT == 2) {
+      const int KS0 = d.KS0;
+      for (int64_t i = 0; i < (int64_t)T * KS0 * 64; ++i) packed[d.w[0] + i] *= kSwishPrescale;
+      for (int l = 0; l < op.n_hidden; ++l)
+        for (int64_t i = 0; i < (int64_t)T * 32; ++i) packed[d.b[l] + i] *= kSwishPrescale;
     }
     // permuted last bias: [pair][o][lane half h][r] = bias[(2 pair + h) S + 16o + r]
     const float* B = nat + op.off_b[op.n_hidden];
