@@ -146,7 +146,7 @@ def spline_kernel_roofline(M, N, K, steps):
         t = float(np.mean([a.elapsed_ms(b) for a, b in evs])) * 1e-3
         if tag == "normalize":  # read + write dx, dy, slope
             nbytes = 2 * M * N * 4 * (3 * K - 1)
-            kname = "normalize_kernel"
+            kname = "normalize_vec_kernel"
         else:
             nbytes = M * (N * (4 * 3 * K + 4) + (4 if tag == "forward" else 0))
             kname = "rqs_kernel_direct" if K in (4, 8, 16, 32) else "rqs_kernel"

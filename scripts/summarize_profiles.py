@@ -21,7 +21,7 @@ OUT = ROOT / "profiles"
 
 def short(name):
     for key in ("flow_kernel_x3<", "flow_kernel<", "rqs_kernel_direct<", "rqs_kernel<", "reduce_partials", "colstats_partial", "colstats_final",
-                "normalize_kernel", "squareplus_kernel", "softmax_threshold_kernel"):
+                "normalize_vec_kernel<", "normalize_kernel", "squareplus_kernel", "softmax_threshold_kernel"):
         if key in name:
             i = name.index(key)
             j = name.find(">", i)

@@ -80,6 +80,27 @@ def test_normalize_and_squareplus_vs_oracle():
     assert_allclose(u.squareplus(a), O.squareplus(a), rtol=1e-5)
 
 
+@pytest.mark.parametrize("K", [2, 4, 5, 8, 16, 32])
+@pytest.mark.parametrize("M", [1, 3, 1023, 4099])
+def test_normalize_spline_params_shapes(K, M):
+    """The float4 stream kernel (K in {4, 8, 16, 32}: ragged tails, rows on
+    K/4 lanes, slope tails) and the LDS row kernel (other K) vs the oracle."""
+    u = _zu()
+    rng = np.random.default_rng(K * 7 + M)
+    a = (3 * rng.standard_normal((M, 2, K))).astype(F32)
+    b = (3 * rng.standard_normal((M, 2, K))).astype(F32)
+    c = (3 * rng.standard_normal((M, 2, K - 1))).astype(F32)
+    got = u.normalize_spline_params(a, b, c)
+    ref = O.normalize_spline_params(a, b, c)
+    # rtol = the north star's 1e-5: x*x + 4 contracts to an fma on the GPU, and
+    # squareplus cancels at large negative logits (a 2-knot row divides two
+    # such values directly: up to ~3e-6 here)
+    for g, r in zip(got, ref):
+        assert g.shape == r.shape
+        assert_allclose(g, r, rtol=1e-5, atol=1e-7)
+    assert_allclose(got[0].sum(-1), 1, rtol=2e-6)
+
+
 @pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8, 16, 32, 64])
 @pytest.mark.parametrize("N", [1, 2, 3, 8])
 def test_rqs_parity(K, N):

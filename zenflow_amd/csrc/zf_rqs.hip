@@ -13,6 +13,8 @@
 #include "zf_internal.h"
 #include "zf_spline.h"
 
+#include <cstdlib>
+
 namespace zf {
 namespace {
 
@@ -235,6 +237,84 @@ __global__ __launch_bounds__(kRowThreads) void normalize_kernel(float* __restric
   }
 }
 
+// normalize_spline_params fast path (K in {4, 8, 16, 32}, 16-B aligned
+// arrays): a pure stream, so every lane moves float4s (1 KiB per
+// wave-instruction, four in flight per lane) and the row of K knots lives on
+// G = K/4 consecutive lanes: lane partial sums (sequential over its four)
+// combined by xor-shuffles.  Quotients by a reciprocal and one fma
+// correction (the correctly rounded quotient but for ties at the last
+// bit; the sum order already makes the result differ from the reference's
+// sequential sum by an ulp).  Blocks [0, B) stream dx, [B, 2B) dy, the rest
+// the slope logits through squareplus.
+constexpr int kNormU = 4;  // float4s per lane
+typedef float nf4 __attribute__((ext_vector_type(4)));
+
+// squareplus with a Newton-corrected hardware rsqrt (x^2 + 4 >= 4: no
+// denormal scaling, unlike sqrtf's expansion): ~0.5 ulp.
+__device__ __forceinline__ float squareplus_stream(float x) {
+  const float a = x * x + 4.0f;
+  const float r = __builtin_amdgcn_rsqf(a);
+  const float sq = a * r;
+  return 0.5f * (x + __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * r, sq));
+}
+
+__device__ __forceinline__ float div_corr(float a, float b, float rb) {
+  const float q = a * rb;
+  return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void normalize_vec_kernel(float* __restrict__ dx, float* __restrict__ dy,
+                                                            float* __restrict__ sl, int64_t n4, int64_t nsl,
+                                                            int64_t bxy, float c, float norm, float rnorm) {
+  constexpr int G = K / 4;
+  const int64_t b = blockIdx.x;
+  if (b < 2 * bxy) {
+    nf4* p = reinterpret_cast<nf4*>(b < bxy ? dx : dy);
+    const int64_t i0 = (b < bxy ? b : b - bxy) * (256 * kNormU) + threadIdx.x;
+    nf4 v[kNormU];
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      const int64_t i = i0 + u * 256;
+      v[u] = i < n4 ? __builtin_nontemporal_load(p + i) : nf4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      nf4 w = v[u];
+      w.x = squareplus_stream(w.x); w.y = squareplus_stream(w.y); w.z = squareplus_stream(w.z); w.w = squareplus_stream(w.w);
+      float sum = ((w.x + w.y) + w.z) + w.w;  // utils.py:32 (jnp.sum over the row)
+#pragma unroll
+      for (int m = 1; m < G; m <<= 1) sum += __shfl_xor(sum, m);
+      const float rs = 1.0f / sum;
+      w.x = div_corr(div_corr(w.x, sum, rs) + c, norm, rnorm);  // utils.py:33
+      w.y = div_corr(div_corr(w.y, sum, rs) + c, norm, rnorm);
+      w.z = div_corr(div_corr(w.z, sum, rs) + c, norm, rnorm);
+      w.w = div_corr(div_corr(w.w, sum, rs) + c, norm, rnorm);
+      const int64_t i = i0 + u * 256;
+      if (i < n4) __builtin_nontemporal_store(w, p + i);
+    }
+  } else {
+    nf4* p = reinterpret_cast<nf4*>(sl);
+    const int64_t n = nsl >> 2;
+    const int64_t i0 = (b - 2 * bxy) * (256 * kNormU) + threadIdx.x;
+    nf4 v[kNormU];
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      const int64_t i = i0 + u * 256;
+      v[u] = i < n ? __builtin_nontemporal_load(p + i) : nf4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      const int64_t i = i0 + u * 256;
+      nf4 w = v[u];
+      w.x = squareplus_stream(w.x); w.y = squareplus_stream(w.y); w.z = squareplus_stream(w.z); w.w = squareplus_stream(w.w);
+      if (i < n) __builtin_nontemporal_store(w, p + i);
+    }
+    if (i0 == 0)  // the < 4 trailing slope logits
+      for (int64_t e = n * 4; e < nsl; ++e) sl[e] = squareplus(sl[e]);
+  }
+}
+
 // utils.py:18-20 elementwise; b is the reference's `b` argument.
 __global__ void squareplus_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
                                   float b) {
@@ -354,6 +434,31 @@ int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, in
   if (M == 0) return ZF_OK;
   if (!dx || !dy || (K > 1 && !slope)) return zf::einval("NULL input");
   if (K > zf::kRowLdsFloats / 2) return zf::einval("K too large");
+  const bool aligned = ((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dy) |
+                         reinterpret_cast<uintptr_t>(slope)) & 15) == 0;
+  if (aligned && (K == 4 || K == 8 || K == 16 || K == 32) && std::getenv("ZF_NORM_ROWS") == nullptr) {
+    const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // utils.py:32 (Python floats)
+    const float norm = (float)(1.0 + c64 * (double)K);
+    const int64_t n4 = M * K / 4, nsl = M * (K - 1);
+    const int64_t per = 256 * zf::kNormU;
+    const int64_t bxy = (n4 + per - 1) / per;
+    int64_t bs = (nsl / 4 + per - 1) / per;
+    if (bs == 0 && nsl > 0) bs = 1;  // tail-only slopes
+    const int64_t grid = 2 * bxy + bs;
+    if (grid > 0x7fffffffLL) return zf::einval("M too large");
+#define ZF_NORMV(KV)                                                                                          \
+  hipLaunchKernelGGL(zf::normalize_vec_kernel<KV>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, dx, \
+                     dy, slope, n4, nsl, bxy, (float)c64, norm, (float)(1.0 / (double)norm))
+    switch (K) {
+      case 4: ZF_NORMV(4); break;
+      case 8: ZF_NORMV(8); break;
+      case 16: ZF_NORMV(16); break;
+      default: ZF_NORMV(32); break;
+    }
+#undef ZF_NORMV
+    ZF_CHECK_LAUNCH("normalize_vec_kernel");
+    return ZF_OK;
+  }
   const int R = zf::rows_per_block(2 * K + 1);  // dx and dy rows share the LDS budget
   const int64_t grid = (M + R - 1) / R;
   if (grid > 0x7fffffffLL) return zf::einval("M too large");

@@ -47,12 +47,25 @@ def softmax_with_threshold(x, threshold: float = 0):
 
 
 def normalize_spline_params(dx, dy, sl) -> Tuple:
-    """utils.py:37-62 — widths/heights via thresholded softmax (EPS), slopes via squareplus."""
-    return (
-        softmax_with_threshold(dx, EPS),
-        softmax_with_threshold(dy, EPS),
-        squareplus(sl),
-    )
+    """utils.py:37-62 — widths/heights via thresholded softmax (EPS), slopes via
+    squareplus.  One launch of ``zf_normalize_spline_params`` over fresh copies
+    (the kernel works in place; host inputs are copied by the upload anyway)."""
+    K = np.shape(dx)[-1]
+    if np.shape(dy) != np.shape(dx) or tuple(np.shape(sl)) != tuple(np.shape(dx)[:-1]) + (K - 1,):
+        raise ValueError(f"dx/dy (..., K) and slope (..., K-1) shapes differ: {np.shape(dx)}, {np.shape(dy)}, {np.shape(sl)}")
+    outs, wases = [], []
+    for a in (dx, dy, sl):
+        ad, was = _dev(a)
+        wases.append(was)
+        if was:  # never write into the caller's device buffer
+            c = DeviceArray(ad.shape)
+            c.copy_from(ad)
+            ad = c
+        outs.append(ad)
+    M = int(np.prod(outs[0].shape[:-1], dtype=np.int64))
+    check(L.load_library().zf_normalize_spline_params(outs[0].ptr, outs[1].ptr, outs[2].ptr, M, K, L.stream()),
+          "zf_normalize_spline_params")
+    return tuple(o if was else o.numpy() for o, was in zip(outs, wases))
 
 
 def _shapes(x, dx, dy, slope):
