@@ -270,19 +270,31 @@ __global__ __launch_bounds__(256) void latent_sample_kernel(int latent, float pa
   z[i] = latent_draw(latent, param, seed, row, d);
 }
 
-// Deterministic fixed-order sum of per-block partials -> out[0].
-__global__ __launch_bounds__(256) void reduce_partials(const double* __restrict__ part, long long n,
-                                                       double* __restrict__ out) {
-  __shared__ double sm[256];
+// Deterministic fixed-order sum of per-block partials -> out[0]: one block
+// of 1024 threads, eight independent loads in flight per thread (the
+// 2^20-row NLL has 8192 partials), then a fixed LDS tree.
+constexpr int kReduceThreads = 1024;
+__global__ __launch_bounds__(kReduceThreads) void reduce_partials(const double* __restrict__ part, long long n,
+                                                                  double* __restrict__ out) {
+  __shared__ double sm[kReduceThreads];
+  const int t = threadIdx.x;
   double acc = 0.0;
-  for (long long i = threadIdx.x; i < n; i += 256) acc += part[i];
-  sm[threadIdx.x] = acc;
+  long long i = t;
+  for (; i + 7 * kReduceThreads < n; i += 8 * kReduceThreads) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = part[i + j * kReduceThreads];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  for (; i < n; i += kReduceThreads) acc += part[i];
+  sm[t] = acc;
   __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if ((int)threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
+  for (int w = kReduceThreads / 2; w >= 1; w >>= 1) {
+    if (t < w) sm[t] += sm[t + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = sm[0];
+  if (t == 0) out[0] = sm[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -706,7 +718,7 @@ int zf_flow_nll_reduce(const void* workspace, int64_t N, double* nll_sum, void* 
     return ZF_OK;
   }
   const long long blocks = (N + zf::kBlockRows - 1) / zf::kBlockRows;
-  hipLaunchKernelGGL(zf::reduce_partials, dim3(1), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(zf::reduce_partials, dim3(1), dim3(zf::kReduceThreads), 0, (hipStream_t)stream,
                      (const double*)workspace, blocks, nll_sum);
   ZF_CHECK_LAUNCH("reduce_partials");
   return ZF_OK;

@@ -82,7 +82,9 @@ struct XT<2> {
 #endif
 
 // Timing-only ablations for tuning builds (results are wrong): 1 no spline
-// math, 2 no block barrier, 3 no MFMA, 4 no swish.
+// math (its dead last-layer MFMAs go too), 2 no block barrier, 3 no MFMA,
+// 4 no swish, 5 no DMA wait and no barrier, 7 spline replaced by a max over
+// its parameters (all MFMAs kept).
 #ifndef ZF_X3_ABLATE
 #define ZF_X3_ABLATE 0
 #endif
@@ -427,8 +429,10 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
                                         int hh, float isc, float us) {
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
+#if ZF_X3_ABLATE != 5
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if ZF_X3_ABLATE != 2
+#endif
+#if ZF_X3_ABLATE != 2 && ZF_X3_ABLATE != 5
   __syncthreads();
 #endif
   X3_MARK(2);
@@ -486,8 +490,10 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   using E = typename XT<NT>::E;
   constexpr int kBuf = group_bytes<NT>(T);
   X3_MARK(1);
+#if ZF_X3_ABLATE != 5
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if ZF_X3_ABLATE != 2
+#endif
+#if ZF_X3_ABLATE != 2 && ZF_X3_ABLATE != 5
   __syncthreads();
 #endif
   X3_MARK(2);
@@ -823,6 +829,14 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
 #if ZF_X3_ABLATE == 1
           yv = xv + P[0] + P[TL * 16 - 1];
           ldv = P[1];
+#elif ZF_X3_ABLATE == 7
+          {
+            float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+            for (int j = 0; j < TL * 16; j += 2) { t0 = fmaxf(t0, P[j]); t1 = fmaxf(t1, P[j + 1]); }
+            yv = xv + t0;
+            ldv = t1;
+          }
 #else
           if (!INV) {
             float l;
