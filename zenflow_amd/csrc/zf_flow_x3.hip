@@ -84,7 +84,7 @@ struct XT<2> {
 // Timing-only ablations for tuning builds (results are wrong): 1 no spline
 // math (its dead last-layer MFMAs go too), 2 no block barrier, 3 no MFMA,
 // 4 no swish, 5 no DMA wait and no barrier, 7 spline replaced by a max over
-// its parameters (all MFMAs kept).
+// its parameters (all MFMAs kept), 8 f16x2 activation scale fixed.
 #ifndef ZF_X3_ABLATE
 #define ZF_X3_ABLATE 0
 #endif
@@ -267,12 +267,16 @@ __device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)
 // hold the same sample.
 template <int T>
 __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius) {
+#if ZF_X3_ABLATE == 8
+  const float m = 16.f;
+#else
   float m = 0.f;
 #pragma unroll
   for (int t = 0; t < T; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
   m = fmaxf(m, __shfl_xor(m, 32));
+#endif
   // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
   // seeded as bias / us stays finite)
   const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
