@@ -151,16 +151,24 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
   if (FWD) {
     float y, l;
     rqs_forward_eval(v, bn, y, l);
-    if (tid < items) {
-      if (out) out[item] = y;
-      s_ld[tid] = l;
-    }
+    if (tid < items && out) out[item] = y;
     if (log_det) {
-      __syncthreads();
-      if (tid < rows) {
-        float acc = 0.f;  // log_det.sum(axis=1), dim order
-        for (int n = 0; n < N; ++n) acc = acc + s_ld[tid * N + n];
-        log_det[r0 + tid] = acc;
+      if (N <= 64 && (N & (N - 1)) == 0) {
+        // a row's N items sit on N consecutive lanes of one wave: gather
+        // them by lane shuffles and sum in dim order (utils.py:139), no LDS
+        // round trip or block barrier
+        const int lane = tid & 63, base = lane & ~(N - 1);
+        float acc = 0.f;
+        for (int n = 0; n < N; ++n) acc = acc + __shfl(l, base + n);
+        if (lane == base && tid < items) log_det[r0 + tid / N] = acc;
+      } else {
+        if (tid < items) s_ld[tid] = l;
+        __syncthreads();
+        if (tid < rows) {
+          float acc = 0.f;  // log_det.sum(axis=1), dim order
+          for (int n = 0; n < N; ++n) acc = acc + s_ld[tid * N + n];
+          log_det[r0 + tid] = acc;
+        }
       }
     }
   } else if (tid < items) {
