@@ -188,6 +188,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-spline-kernel", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="RCCL all-reduce even at world size 1 (plumbing check)")
+    ap.add_argument("--serial-allreduce", action="store_true",
+                    help="NLL all-reduce on the compute stream after every step (no overlap)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,7 +207,7 @@ def main():
     import zenflow_amd as zf
     from zenflow_amd import _lib as L
     from zenflow_amd._lib import DeviceArray, Event
-    from zenflow_amd.dist import RcclCommunicator
+    from zenflow_amd.dist import OverlappedAllreduce, RcclCommunicator
     from zenflow_amd.random import PRNGKey
 
     L.ensure_device()
@@ -245,6 +247,9 @@ def main():
             return obj[0]
 
         comm = RcclCommunicator(rank, world, bcast)
+    # the NLL all-reduce runs on a communication stream beside the next
+    # step's kernel (double-buffered partial; dist.OverlappedAllreduce)
+    ar = OverlappedAllreduce(comm) if comm is not None and not args.serial_allreduce else None
 
     n_ops = len(prog.ops)
     events = []
@@ -257,9 +262,13 @@ def main():
                                                  None, out.ptr, None, ws.ptr, N, L.stream()), "log_prob")
             if ev is not None:
                 ev[1].record()
-            L.check(lib.zf_flow_nll_reduce(ws.ptr, N, nll.ptr, L.stream()), "nll_reduce")
-            if comm is not None:
-                comm.allreduce_sum_(nll)
+            if ar is not None:
+                L.check(lib.zf_flow_nll_reduce(ws.ptr, N, ar.buffer().ptr, L.stream()), "nll_reduce")
+                ar.launch()
+            else:
+                L.check(lib.zf_flow_nll_reduce(ws.ptr, N, nll.ptr, L.stream()), "nll_reduce")
+                if comm is not None:
+                    comm.allreduce_sum_(nll)
         elif mode == "sample":
             if ev is not None:
                 ev[0].record()
@@ -273,16 +282,19 @@ def main():
             if ev is not None:
                 ev[1].record()
 
+    def sync_all():  # the library stream and, with overlap, the comm stream
+        L.check(lib.zf_device_synchronize(), "device_synchronize")
+
     for _ in range(args.warmup):
         step()
-    L.synchronize()
+    sync_all()
     evs = [(Event(), Event()) for _ in range(args.steps)]
     barrier()
-    L.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(evs[i])
-    L.synchronize()
+    sync_all()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -342,7 +354,8 @@ def main():
         },
     }
     if mode == "log_prob":
-        result["nll"] = -float(nll.numpy()[0]) / (N * world)
+        nll_buf = ar.last if ar is not None and ar.last is not None else nll
+        result["nll"] = -float(nll_buf.numpy()[0]) / (N * world)
     if not args.no_spline_kernel:
         result["spline_kernel"] = spline_kernel_roofline(N, 2, K, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -57,6 +57,8 @@ int zf_event_destroy(void* event);
 int zf_event_record(void* event, void* stream);
 int zf_event_elapsed_ms(void* start, void* stop, float* ms);
 int zf_event_synchronize(void* event);
+/* Work queued on `stream` after this call waits for `event` (hipStreamWaitEvent). */
+int zf_stream_wait_event(void* stream, void* event);
 
 /* ------------------------------------------------------------------------ */
 /* K1 — spline numerics at the `zenflow.utils` boundary.                     */

@@ -97,6 +97,7 @@ SIGNATURES = {
     "zf_event_create": (_int, [C.POINTER(_vp)]),
     "zf_event_destroy": (_int, [_vp]),
     "zf_event_record": (_int, [_vp, _vp]),
+    "zf_stream_wait_event": (_int, [_vp, _vp]),
     "zf_event_elapsed_ms": (_int, [_vp, _vp, C.POINTER(C.c_float)]),
     "zf_event_synchronize": (_int, [_vp]),
     "zf_rqs_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp]),
@@ -218,6 +219,14 @@ def stream():
     return _stream
 
 
+def new_stream():
+    """A further HIP stream on this process's device (e.g. for communication)."""
+    ensure_device()
+    s = C.c_void_p()
+    check(load_library().zf_stream_create(C.byref(s)), "zf_stream_create")
+    return s.value
+
+
 def synchronize() -> None:
     check(load_library().zf_stream_synchronize(stream()), "zf_stream_synchronize")
 
@@ -322,6 +331,10 @@ class Event:
 
     def synchronize(self):
         check(load_library().zf_event_synchronize(self.ptr), "event_sync")
+
+    def wait(self, s=None):
+        """Make work queued later on stream `s` (default: the library stream) wait for this event."""
+        check(load_library().zf_stream_wait_event(stream() if s is None else s, self.ptr), "stream_wait_event")
 
     def elapsed_ms(self, end: "Event") -> float:
         ms = C.c_float()

@@ -121,6 +121,12 @@ int zf_event_destroy(void* event) {
   return ZF_OK;
 }
 
+int zf_stream_wait_event(void* stream, void* event) {
+  if (!event) return zf::einval("event is NULL");
+  ZF_TRY_HIP(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+  return ZF_OK;
+}
+
 int zf_event_record(void* event, void* stream) {
   ZF_TRY_HIP(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
   return ZF_OK;

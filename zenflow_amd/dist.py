@@ -48,12 +48,13 @@ class RcclCommunicator:
         self.comm = comm.value
         self.rank, self.world = rank, world
 
-    def allreduce_sum_(self, buf: DeviceArray) -> DeviceArray:
-        """In-place fp64 sum across ranks on the library stream."""
+    def allreduce_sum_(self, buf: DeviceArray, stream=None) -> DeviceArray:
+        """In-place fp64 sum across ranks on ``stream`` (default: the library stream)."""
         if buf.dtype != np.float64:
             raise TypeError("fp64 buffer expected")
         check(L.load_library().zf_rccl_allreduce_sum_f64(
-            self.comm, buf.ptr, buf.ptr, buf.shape[0] if buf.shape else 1, L.stream()), "allreduce")
+            self.comm, buf.ptr, buf.ptr, buf.shape[0] if buf.shape else 1,
+            L.stream() if stream is None else stream), "allreduce")
         return buf
 
     def close(self):
@@ -83,6 +84,48 @@ class GlooCommunicator:
 def nll_from_sum(total_sum: float, n_total: int) -> float:
     """-mean(log_prob) (train.py:78) from the all-reduced fp64 sum."""
     return float(-total_sum / max(1, n_total))
+
+
+class OverlappedAllreduce:
+    """All-reduce of a per-step fp64 partial on a communication stream, off
+    the compute stream's critical path: step i's reduce output (slot i of a
+    ring of buffers) is handed to the comm stream by an event, and the
+    compute stream waits only when it comes back to a slot — ``depth`` steps
+    later — for the all-reduce that last read it.  Ranks are thus not put in
+    lockstep by every step's collective; the caller synchronises the device
+    at the end."""
+
+    def __init__(self, comm: RcclCommunicator, count: int = 1, depth: int = 64):
+        from ._lib import Event
+
+        self.comm = comm
+        self.depth = depth
+        self.stream = L.new_stream()
+        self.bufs = [DeviceArray((count,), np.float64) for _ in range(depth)]
+        self.ready = [Event() for _ in range(depth)]
+        self.done = [Event() for _ in range(depth)]
+        self.pending = [False] * depth
+        self.i = 0
+        self.last = None
+
+    def buffer(self) -> DeviceArray:
+        """The buffer this step's partial goes into (on reuse of a slot the
+        compute stream first waits for the slot's previous all-reduce)."""
+        k = self.i % self.depth
+        if self.pending[k]:
+            self.done[k].wait()
+        return self.bufs[k]
+
+    def launch(self) -> None:
+        """All-reduce this step's buffer once the compute stream has filled it."""
+        k = self.i % self.depth
+        self.ready[k].record()
+        self.ready[k].wait(self.stream)
+        self.comm.allreduce_sum_(self.bufs[k], stream=self.stream)
+        self.done[k].record(self.stream)
+        self.pending[k] = True
+        self.last = self.bufs[k]
+        self.i += 1
 
 
 class ShardedLogProb:
