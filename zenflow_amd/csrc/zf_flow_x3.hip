@@ -487,6 +487,11 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 #ifndef ZF_X3_PIPE_VALU
 #define ZF_X3_PIPE_VALU 0
 #endif
+// Tuning: wave priority by phase — 1: 1 in the weight-group (MFMA) phases,
+// 0 elsewhere; 2: the reverse (spline / layer 0 / epilogue at priority 1).
+#ifndef ZF_X3_PRIO
+#define ZF_X3_PRIO 0
+#endif
 template <int NT, int T, int NOUT, int Q, bool HASB>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
@@ -501,6 +506,9 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   __syncthreads();
 #endif
   X3_MARK(2);
+#if ZF_X3_PRIO
+  __builtin_amdgcn_s_setprio(ZF_X3_PRIO == 2 ? 0 : 1);
+#endif
   x3_issue_next<NT, T>(x3, p, p.wbuf + (p.buf ^ 1) * kBuf, lane);
   floatx16 bt[NOUT];
   if constexpr (HASB) {
@@ -554,6 +562,9 @@ __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pip
     x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
   } else {
     x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+#if ZF_X3_PRIO
+    __builtin_amdgcn_s_setprio(ZF_X3_PRIO == 2 ? 1 : 0);
+#endif
   }
 }
 
