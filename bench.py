@@ -194,6 +194,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 as "
+              f"`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N` "
+              f"(one process per GPU); running on {world} GPU(s)", file=sys.stderr)
     td = None
     if world > 1:
         import torch.distributed as td
