@@ -21,6 +21,10 @@ CONFIGS = {
     "odd": dict(D=5, C=3, K=7, layers=(48, 96, 32), latent="truncated_normal"),
     "uniform": dict(D=2, C=0, K=4, layers=(32,), latent="uniform"),
     "deep": dict(D=2, C=8, K=16, layers=(128,) * 6, latent="beta"),  # deep_set NB shape
+    # one transformed dim on the split-MFMA kernel's one-dim last-layer layout:
+    # hidden 128 with dc = 2 and a condition; hidden 256 (dim-pair path)
+    "d3c1": dict(D=3, C=1, K=16, layers=(128, 128), latent="normal"),
+    "d2h256": dict(D=2, C=0, K=32, layers=(256, 256), latent="normal"),
 }
 
 

@@ -46,7 +46,7 @@ def check_lp(lp, case, tag=""):
     return err.max()
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"])
 @pytest.mark.parametrize("N", [1, 1000, 4096])
 def test_log_prob_parity(name, N):
     case = make_case(name, N=N, seed=11)
@@ -58,7 +58,7 @@ def test_log_prob_parity_cfg5():
     check_lp(gpu_log_prob(case), case, "cfg5")
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"])
 def test_inverse_parity(name):
     case = make_case(name, N=2000, seed=13)
     rng = np.random.default_rng(7)
@@ -74,7 +74,7 @@ def test_inverse_parity(name):
     assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
 
 
-@pytest.mark.parametrize("name", ["cfg2", "odd"])
+@pytest.mark.parametrize("name", ["cfg2", "odd", "cfg4", "d3c1", "d2h256"])
 def test_chain_forward_parity(name):
     """Chain.__call__ (y, log_det) vs the oracle's chain."""
     case = make_case(name, N=3000, seed=14)
@@ -204,7 +204,7 @@ def test_edge_inputs():
 # ZF_DISABLE_X3=1 the fp32-MFMA kernel, which must stay parity-green on the
 # same shapes.
 
-X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5"]
+X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"]
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"])

@@ -646,7 +646,12 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // footprint is 2 groups + the state: 50 KiB at T = 4 (3 blocks = 3 waves per
 // SIMD, <= 168 VGPRs), 104 KiB at T = 8 (hidden 256: one block per CU, the
 // 8 + 8 accumulator tiles need one wave's whole register file).
-template <int NT, int K, int T, bool PAIRS, bool INV>
+// ONE (one transformed dim, dim 2 or 3): the last layer's rows carry that
+// dim's parameters in both lane halves (tile o, half h, register r =
+// parameter 32o + 16h + r), so it takes ceil((3K-1)/32) tiles instead of
+// ceil((3K-1)/16) half-empty ones, and the halves swap theirs by a lane
+// shuffle before the spline.
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV>
 #ifndef ZF_X3_NARROW_OCC
 #define ZF_X3_NARROW_OCC 3
 #endif
@@ -656,7 +661,9 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
     double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N,
     unsigned long long seed, int gen) {
-  constexpr int TL = (3 * K - 1 + 15) / 16;  // last-layer tiles per dim pair: 16 parameters per lane half
+  // last-layer tiles per dim pair: 16 parameters per lane half (ONE: 32 of one dim per tile)
+  constexpr int TL = ONE ? (3 * K - 1 + 31) / 32 : (3 * K - 1 + 15) / 16;
+  constexpr int NPV = ONE ? 32 * TL : 16 * TL;  // spline parameters held per lane
   constexpr int NW = kX3Waves;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int D = F->D;
@@ -803,11 +810,19 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
           for (int o = 0; o < TL; ++o) pa[o] *= lus;
         }
         X3_MARK(7);
-        float P[TL * 16];
+        float P[NPV];
 #pragma unroll
         for (int o = 0; o < TL; ++o)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) P[16 * o + r] = pa[o][r];
+          for (int r = 0; r < 16; ++r) {
+            if constexpr (ONE) {  // both halves end up with all of the dim's parameters
+              const float other = __shfl_xor(pa[o][r], 32);
+              P[32 * o + r] = hh == 0 ? pa[o][r] : other;
+              P[32 * o + 16 + r] = hh == 0 ? other : pa[o][r];
+            } else {
+              P[16 * o + r] = pa[o][r];
+            }
+          }
         // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
         const int d = 2 * pr + hh;
         const bool act = d < dt;  // the upper half idles on an odd last dim
@@ -842,13 +857,13 @@ __global__ __launch_bounds__(kX3Waves * 64, T == 4 ? ZF_X3_NARROW_OCC : 1) void 
                                                        [](float v) { return v == 0.f ? 1.f : x3_squareplus(v); });
           float yv;
 #if ZF_X3_ABLATE == 1
-          yv = xv + P[0] + P[TL * 16 - 1];
+          yv = xv + P[0] + P[NPV - 1];
           ldv = P[1];
 #elif ZF_X3_ABLATE == 7
           {
             float t0 = 0.f, t1 = 0.f;
 #pragma unroll
-            for (int j = 0; j < TL * 16; j += 2) { t0 = fmaxf(t0, P[j]); t1 = fmaxf(t1, P[j + 1]); }
+            for (int j = 0; j < NPV; j += 2) { t0 = fmaxf(t0, P[j]); t1 = fmaxf(t1, P[j + 1]); }
             yv = xv + t0;
             ldv = t1;
           }
@@ -926,6 +941,8 @@ int x3_scheme() {
 }
 
 int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
+// ONE layout (one transformed dim): 32 parameters per tile
+int x3_last_tiles_one(int K) { return (3 * K - 1 + 31) / 32; }
 
 int x3_pairs(const zf_flow_desc& desc) { return (desc.dim / 2 + 1) / 2; }
 
@@ -947,7 +964,8 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
     if (op.kind != ZF_OP_NSC) continue;
     DevOp& d = F.ops[i];
     const int dt = desc.dim / 2, K = op.knots, S = 3 * K - 1;
-    const int TL = x3_last_tiles(K), NP = x3_pairs(desc);
+    const bool one = dt == 1;
+    const int TL = one ? x3_last_tiles_one(K) : x3_last_tiles(K), NP = x3_pairs(desc);
     d.x3 = (long long)stream.size() * 2;
     d.x3_tlast = TL;
     d.x3_groups = T * (op.n_hidden - 1) + T * NP;
@@ -986,8 +1004,9 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
                     col = 32 * o + rho;
                     if (col >= out) col = -1;
                   } else {
-                    const int h = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3), jp = 16 * o + r;
-                    const int dd = 2 * pr + h;
+                    const int h = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3);
+                    const int jp = one ? 32 * o + 16 * h + r : 16 * o + r;
+                    const int dd = one ? 0 : 2 * pr + h;
                     col = (dd < dt && jp < S) ? dd * S + jp : -1;
                   }
                   const float x = (k < in && col >= 0) ? W[(int64_t)k * out + col] : 0.f;
@@ -1025,7 +1044,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
       for (int o = 0; o < TL; ++o)
         for (int h = 0; h < 2; ++h)
           for (int r = 0; r < 16; ++r) {
-            const int jp = 16 * o + r, dd = 2 * pr + h;
+            const int jp = one ? 32 * o + 16 * h + r : 16 * o + r, dd = one ? 0 : 2 * pr + h;
             packed[d.x3_blast + ((pr * TL + o) * 2 + h) * 16 + r] = (dd < dt && jp < S) ? B[dd * S + jp] : 0.f;
           }
   }
@@ -1035,7 +1054,7 @@ size_t x3_lds_bytes(int T, int D, int NT) {
   return (size_t)2 * 2 * T * NT * 1024 + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
 }
 
-template <int NT, int K, int T, bool PAIRS>
+template <int NT, int K, int T, bool PAIRS, bool ONE>
 int launch_x3(const X3Launch& a, bool inverse) {
   const long long rows = kX3Waves * kTile;
   const long long grid = (a.N + rows - 1) / rows;
@@ -1043,11 +1062,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
   const size_t lds = x3_lds_bytes(T, a.D, NT);
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
@@ -1058,10 +1077,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
 // (cfg1-4, deep-set); hidden <= 256 with K 16/32, any dt <= 8 (cfg5).
 template <int NT>
 int launch_x3_nt(const X3Launch& a, bool inverse) {
-  if (a.T == 4 && a.K == 8) return launch_x3<NT, 8, 4, false>(a, inverse);
-  if (a.T == 4 && a.K == 16) return launch_x3<NT, 16, 4, false>(a, inverse);
-  if (a.T == 8 && a.K == 16) return launch_x3<NT, 16, 8, true>(a, inverse);
-  if (a.T == 8 && a.K == 32) return launch_x3<NT, 32, 8, true>(a, inverse);
+  const bool one = a.D / 2 == 1;  // must match x3_pack's last-layer layout
+  if (a.T == 4 && a.K == 8) return one ? launch_x3<NT, 8, 4, false, true>(a, inverse) : launch_x3<NT, 8, 4, false, false>(a, inverse);
+  if (a.T == 4 && a.K == 16) return one ? launch_x3<NT, 16, 4, false, true>(a, inverse) : launch_x3<NT, 16, 4, false, false>(a, inverse);
+  if (a.T == 8 && a.K == 16) return one ? launch_x3<NT, 16, 8, true, true>(a, inverse) : launch_x3<NT, 16, 8, true, false>(a, inverse);
+  if (a.T == 8 && a.K == 32) return one ? launch_x3<NT, 32, 8, true, true>(a, inverse) : launch_x3<NT, 32, 8, true, false>(a, inverse);
   return enotsup("split-MFMA kernel: shape not instantiated");
 }
 
