@@ -122,6 +122,27 @@ def _take_fill(arr, idx):
     return np.where(ok[..., 0], out, np.asarray(np.nan, dtype=arr.dtype))
 
 
+# Rows whose spline input lies in the last-knot sliver band [1 - SLIVER, 1):
+# there the fp32 knot sum (which can end slightly below 1) decides whether
+# idx == K (fill-mode NaN, Appendix A.4), so two fp32 evaluations with
+# different summation orders may legitimately disagree on finiteness.
+SLIVER = 1e-5
+_SLIVER_LOG: Dict[str, Any] = {"rows": None}
+
+
+def sliver_rows(fn, *args, **kwargs):
+    """Run ``fn`` and return (its result, bool mask of rows that touched the
+    sliver band in any coupling).  Rows are axis 0 of every spline input."""
+    _SLIVER_LOG["rows"] = None
+    _SLIVER_LOG["on"] = True
+    try:
+        out = fn(*args, **kwargs)
+    finally:
+        _SLIVER_LOG["on"] = False
+    rows = _SLIVER_LOG["rows"]
+    return out, rows
+
+
 def compute_rqs_input(x, dx, dy, slope, forward):
     """utils.py:205-232."""
     dt = dx.dtype
@@ -131,6 +152,11 @@ def compute_rqs_input(x, dx, dy, slope, forward):
     dk = np.concatenate([one, slope, one], axis=-1)  # :211-216
     sk = dy / dx  # :218
     idx, oob = index(x, xk if forward else yk)
+    if _SLIVER_LOG.get("on"):
+        band = (x >= 1 - SLIVER) & (x < 1)
+        band = band.reshape(band.shape[0], -1).any(axis=1)
+        prev = _SLIVER_LOG["rows"]
+        _SLIVER_LOG["rows"] = band if prev is None else (prev | band)
     return (
         _take_fill(xk, idx),
         _take_fill(yk, idx),
@@ -500,10 +526,31 @@ def flow_log_prob(model, variables, x, c=None, train=False, dtype=np.float32):
         c = c.astype(dtype)
     z, ld, ns = bijector_forward(model["bijector"], params, stats, x, c, train, dtype)
     lp = latent_log_prob(model["latent"], z) + ld  # :46
-    # :47 jnp.nan_to_num(nan=-inf): +inf -> max finite, -inf -> min finite
-    fi = np.finfo(lp.dtype)
-    lp = np.nan_to_num(lp, nan=-np.inf, posinf=fi.max, neginf=fi.min)
+    lp = jnp_nan_to_num(lp, nan=-np.inf)  # :47
     return lp, ns
+
+
+def jnp_nan_to_num(x, nan=0.0):
+    """``jax.numpy.nan_to_num(x, nan=nan)`` for a real floating array (flow.py:47).
+
+    JAX's published implementation (jax/_src/numpy: ``nan_to_num``) is a
+    sequential ``where`` chain on the RUNNING result, with posinf/neginf
+    defaulting to ``finfo(dtype).max/.min``::
+
+        out = where(isnan(x), nan, x)
+        out = where(isposinf(out), posinf, out)
+        out = where(isneginf(out), neginf, out)
+
+    so with ``nan=-inf`` a NaN row first becomes -inf and then
+    ``finfo.min`` (-3.4028235e38 in fp32).  NumPy's ``np.nan_to_num`` takes
+    all three masks from the INPUT instead (NaN would stay -inf), which is
+    why this is spelled out rather than delegated."""
+    x = np.asarray(x)
+    fi = np.finfo(x.dtype)
+    out = np.where(np.isnan(x), np.asarray(nan, x.dtype), x)
+    out = np.where(np.isposinf(out), fi.max, out)
+    out = np.where(np.isneginf(out), fi.min, out)
+    return out.astype(x.dtype)
 
 
 def flow_inverse(model, variables, z, c=None, dtype=np.float32):
@@ -539,6 +586,21 @@ def row_sensitivity(model, variables, x, c=None, reps=4, eps=2.0**-22, seed=0):
 
 
 def nll(log_prob):
-    """train.py:75-78 — -mean(log_prob), accumulated in fp64."""
+    """train.py:75-78 — -jnp.mean(log_prob) of an fp32 array.
+
+    Accumulated in fp64 (a defined order), with the reference's fp32 overflow
+    kept: ``jnp.mean`` sums in fp32, so a batch whose sum leaves the fp32
+    range — e.g. two rows at finfo.min after flow.py:47 — has an infinite
+    NLL there (and train.py:124-127 aborts)."""
     lp = np.asarray(log_prob, dtype=np.float64)
-    return float(-lp.sum() / max(1, lp.shape[0]))
+    return nll_from_sum(float(lp.sum()), lp.shape[0])
+
+
+def nll_from_sum(total, n):
+    """-total/n, infinite where the fp32 sum would overflow (see ``nll``)."""
+    if total != total:
+        return float("nan")
+    with np.errstate(over="ignore"):
+        if not np.isfinite(np.float32(total)):
+            return float("inf") if total < 0 else float("-inf")
+    return float(-total / max(1, n))

@@ -61,9 +61,40 @@ def inverse_fixture():
     np.savez_compressed(OUT / "flow_cfg3_inverse.npz", z=z, x=x, x64=x64, meta=np.array(meta))
 
 
+def edge_fixtures():
+    """flow_edges_<cfg>.npz: flow.py:47 on NaN rows and on rows clipped to the
+    ShiftBounds edges.  jnp.nan_to_num(nan=-inf) maps NaN -> -inf -> finfo.min
+    and a Beta latent at its support edge (z == 1 after the clip) gives -inf ->
+    finfo.min; with two or more such rows the fp32 NLL sum overflows (inf)."""
+    for name, seed in [("cfg1", 201), ("cfg2", 202), ("cfg4", 204)]:
+        N = 64
+        case = make_case(name, N=N, seed=seed)
+        x = case["x"].copy()
+        sb = case["variables"]["batch_stats"]["bijector"]["bijectors_0"]
+        D = x.shape[1]
+        xmin = np.array([sb[f"xmin_{i}"][0] for i in range(D)], np.float32)
+        xmax = np.array([sb[f"xmax_{i}"][0] for i in range(D)], np.float32)
+        x[0, 0] = np.nan
+        x[1, :] = np.nan
+        x[2, :] = 1e30  # clips to z = 1 in every dim
+        x[3, :] = -1e30  # clips to z = 0
+        x[4, :] = xmax
+        x[5, :] = xmin
+        x[6, :] = np.inf
+        x[7, :] = -np.inf
+        x[8, -1] = np.nan  # NaN in a conditioning column only
+        lp, _ = O.flow_log_prob(case["model"], case["variables"], x, case["c"])
+        fin = np.abs(lp) < 1e38
+        meta = json.dumps({"name": name, "N": N, "seed": seed})
+        extra = {} if case["c"] is None else {"c": case["c"]}
+        np.savez_compressed(OUT / f"flow_edges_{name}.npz", x=x, log_prob=lp, nll=np.float64(O.nll(lp)),
+                            nll_finite=np.float64(O.nll(lp[fin])), meta=np.array(meta), **extra)
+
+
 if __name__ == "__main__":
     rqs_fixtures()
     flow_fixtures()
     inverse_fixture()
+    edge_fixtures()
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

@@ -1,10 +1,12 @@
 """Fused flow kernel parity: zenflow_amd Flow/Chain (one HIP launch) vs the oracle,
 at every BASELINE.json config shape, plus full-size properties.  Needs the GPU.
 
-Tolerance (north star: 1e-5 relative fp32): per sample
-|gpu - oracle32| <= 1e-5 * max(1, |oracle64|), and the GPU's error against the
-fp64 oracle must not exceed 2x the fp32 oracle's own error + 2e-6 (both are
-fp32 evaluations of the same graph with different rounding orders)."""
+Tolerance (north star: 1e-5 relative fp32).  ``check_lp``: per row
+|gpu - oracle64| <= 1e-5 max(1, |oracle64|) + 2 (|oracle32 - oracle64| + the
+row's conditioning), finiteness identical off the last-knot sliver.
+``_assert_strict`` (test_strict_parity, test_trained_weights_parity): the
+unwidened |gpu - oracle32| <= 1e-5 max(1, |oracle32|) on every
+well-conditioned row, and on every row |gpu - oracle64| <= 1e-5 + conditioning."""
 
 import numpy as np
 import pytest
@@ -23,17 +25,40 @@ def gpu_log_prob(case):
     return flow.apply(case["variables"], case["x"], case["c"])
 
 
+def strict_rel_err(lp, ref32):
+    """north_star's bar as written: max |gpu - oracle32| / max(1, |oracle32|)
+    over the rows where both are finite (|v| < 1e38)."""
+    f = np.isfinite(ref32) & np.isfinite(lp) & (np.abs(ref32) < 1e38) & (np.abs(lp) < 1e38)
+    if not f.any():
+        return 0.0
+    return float((np.abs(lp[f].astype(np.float64) - ref32[f]) / np.maximum(1.0, np.abs(ref32[f]))).max())
+
+
 def check_lp(lp, case, tag=""):
-    ref32, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float32)
-    ref64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float64)
+    """Per-row parity of ``lp`` with the oracle.
+
+    * Finiteness must agree on every row except those the oracle flags as
+      touching the last-knot sliver (idx == K depends on the fp32 knot sum).
+    * |gpu - oracle64| <= 1e-5 max(1, |oracle64|) + 2 (|oracle32 - oracle64| +
+      row sensitivity): the fp32 bar widened by the conditioning every fp32
+      evaluation (the reference's included) is subject to."""
+    (ref32, _), sl32 = O.sliver_rows(O.flow_log_prob, case["model"], case["variables"], case["x"], case["c"],
+                                     dtype=np.float32)
+    (ref64, _), sl64 = O.sliver_rows(O.flow_log_prob, case["model"], case["variables"], case["x"], case["c"],
+                                     dtype=np.float64)
     assert lp.shape == ref32.shape and lp.dtype == np.float32
     scale = np.maximum(1.0, np.abs(ref64))
     fin32 = np.isfinite(ref32) & (np.abs(ref32) < 1e38)
     fin_gpu = np.isfinite(lp) & (np.abs(lp) < 1e38)
-    # A row can only disagree on finiteness through the idx == K sliver (an
-    # fp32 knot-sum rounding); those must be rare.
-    mismatch = fin32 != fin_gpu
-    assert mismatch.mean() <= 1e-3, f"{tag}: {mismatch.sum()} finiteness mismatches"
+    sliver = np.zeros(lp.shape, bool)
+    for s in (sl32, sl64):
+        if s is not None:
+            sliver |= s
+    mismatch = (fin32 != fin_gpu) & ~sliver
+    assert not mismatch.any(), f"{tag}: {mismatch.sum()} finiteness mismatches off the sliver band"
+    # non-finite rows: the same flow.py:47 value (finfo.min / finfo.max)
+    nf = ~fin32 & ~fin_gpu
+    assert np.array_equal(lp[nf], ref32[nf]), f"{tag}: non-finite rows differ"
     both = fin32 & fin_gpu & np.isfinite(ref64)
     sens = O.row_sensitivity(case["model"], case["variables"], case["x"], case["c"])
     e_o32 = np.abs(ref32[both].astype(np.float64) - ref64[both])
@@ -180,8 +205,12 @@ def test_determinism():
     assert np.array_equal(a, b, equal_nan=True)
 
 
+FMIN = float(np.finfo(np.float32).min)
+
+
 def test_edge_inputs():
-    """NaN rows -> -inf (flow.py:47), huge inputs clip, empty batch."""
+    """NaN rows -> finfo.min (jnp.nan_to_num(nan=-inf), flow.py:47, JAX's
+    sequential where chain), huge inputs clip, empty batch."""
     case = make_case("cfg2", N=64, seed=23)
     x = case["x"].copy()
     x[3, 1] = np.nan
@@ -190,11 +219,41 @@ def test_edge_inputs():
     case["x"] = x
     lp = gpu_log_prob(case)
     ref, _ = O.flow_log_prob(case["model"], case["variables"], x, None)
-    assert lp[3] == -np.inf and ref[3] == -np.inf
-    fin = np.isfinite(ref)
+    assert lp[3] == FMIN and ref[3] == FMIN
+    fin = np.isfinite(ref) & (np.abs(ref) < 1e38)
     assert_allclose(lp[fin], ref[fin], rtol=REL, atol=REL)
     case["x"] = np.zeros((0, 4), F32)
     assert gpu_log_prob(case).shape == (0,)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_golden_edges(name):
+    """tests/golden/flow_edges_<cfg>.npz: NaN rows, rows clipped to the
+    ShiftBounds edges (Beta support edge z = 1 -> -inf -> finfo.min), and
+    the NLL of the batch (infinite: two finfo.min rows overflow the fp32 sum)."""
+    import json
+    from pathlib import Path
+
+    from zenflow_amd._lib import DeviceArray
+    from zenflow_amd.dist import nll_from_sum
+
+    d = np.load(Path(__file__).parent / "golden" / f"flow_edges_{name}.npz")
+    meta = json.loads(str(d["meta"]))
+    case = make_case(meta["name"], N=int(meta["N"]), seed=int(meta["seed"]))
+    flow, bf = _bound(case)
+    xd = DeviceArray.from_numpy(d["x"])
+    cd = DeviceArray.from_numpy(d["c"]) if "c" in d.files else None
+    nll = DeviceArray((1,), np.float64)
+    lp = bf.log_prob(xd, cd, nll_sum=nll).numpy()
+    ref = d["log_prob"]
+    edge = np.abs(ref) >= 1e38
+    assert edge.sum() >= 2
+    assert np.array_equal(lp[edge], ref[edge])
+    f = ~edge
+    assert_allclose(lp[f], ref[f], rtol=REL, atol=REL * np.maximum(1, np.abs(ref[f])).max())
+    assert nll_from_sum(nll.numpy()[0], lp.shape[0]) == float(d["nll"])
+    # the finite part of the batch has the finite NLL
+    assert nll_from_sum(lp[f].astype(np.float64).sum(), f.sum()) == pytest.approx(float(d["nll_finite"]), rel=REL)
 
 
 # --- kernel variants -----------------------------------------------------------
@@ -297,3 +356,94 @@ def test_x3_matches_fp32_kernel(monkeypatch):
     assert np.mean(np.isfinite(l3) != np.isfinite(l32)) <= 1e-3
     rel = np.abs(l3[fin] - l32[fin]) / np.maximum(1, np.abs(l32[fin]))
     assert np.quantile(rel, 0.999) <= REL and rel.mean() <= 1e-6
+
+
+# --- strict per-config bar ------------------------------------------------------
+STRICT_CONFIGS = ["cfg1", "cfg2", "cfg4", "cfg4c1", "cfg5", "d3c1"]
+
+
+WELL_CONDITIONED = 2.5e-6  # row_sensitivity / max(1, |lp|) at ~4 fp32 ulp of injected noise
+
+
+def _strict_record(name, lp, case, scheme):
+    """Strict numbers of one run (appended to gpurun_out/strict_parity.jsonl).
+
+    ``strict_*`` is north_star's max |gpu - oracle32| / max(1, |oracle32|).
+    Rows are split by conditioning: a row whose log_prob moves by more than
+    WELL_CONDITIONED (relative) when ~4 ulp of noise is injected into every
+    fp32 intermediate (oracle.row_sensitivity) cannot be pinned to 1e-5 of
+    ANOTHER fp32 evaluation by any implementation — the reference's own XLA
+    order included — so there the yardstick is fp64 and the row's conditioning."""
+    ref32, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float32)
+    ref64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], dtype=np.float64)
+    sens = O.row_sensitivity(case["model"], case["variables"], case["x"], case["c"])
+    f = (np.abs(ref32) < 1e38) & (np.abs(lp) < 1e38) & np.isfinite(ref64) & (np.abs(ref64) < 1e300)
+    sc = np.maximum(1.0, np.abs(ref64[f]))
+    e_g = np.abs(lp[f] - ref64[f]) / sc
+    e_o = np.abs(ref32[f] - ref64[f]) / sc
+    s_r = sens[f] / sc
+    e_s = np.abs(lp[f].astype(np.float64) - ref32[f]) / np.maximum(1.0, np.abs(ref32[f]))
+    wc = s_r <= WELL_CONDITIONED
+    rec = {"config": name, "scheme": scheme, "rows": int(f.sum()),
+           "strict_max_rel_err_vs_oracle32": float(e_s.max()),
+           "well_conditioned_rows": int(wc.sum()),
+           "strict_max_rel_err_vs_oracle32_well_conditioned": float(e_s[wc].max()) if wc.any() else 0.0,
+           "gpu_max_rel_err_vs_fp64": float(e_g.max()), "oracle32_max_rel_err_vs_fp64": float(e_o.max()),
+           "gpu_mean_rel_err_vs_fp64": float(e_g.mean()), "oracle32_mean_rel_err_vs_fp64": float(e_o.mean()),
+           "max_err_over_conditioning": float((e_g / (REL + s_r)).max())}
+    _append_record("strict_parity.jsonl", rec)
+    return rec
+
+
+def _append_record(fname, rec):
+    import json
+    import os
+    from pathlib import Path
+
+    d = Path(os.environ.get("GRAFT_REPO_ROOT", Path(__file__).resolve().parents[1])) / "gpurun_out"
+    d.mkdir(exist_ok=True)
+    with open(d / fname, "a") as fh:
+        fh.write(json.dumps(rec) + "\n")
+
+
+def _assert_strict(rec):
+    """1e-5 of the fp32 oracle on every well-conditioned row; every row within
+    1e-5 + its conditioning of fp64; mean error no worse than the fp32 oracle's."""
+    tag = f"{rec['scheme']}/{rec['config']}"
+    assert rec["well_conditioned_rows"] > 0, tag
+    assert rec["strict_max_rel_err_vs_oracle32_well_conditioned"] <= REL, tag
+    assert rec["max_err_over_conditioning"] <= 1.0, tag
+    assert rec["gpu_mean_rel_err_vs_fp64"] <= 1.25 * rec["oracle32_mean_rel_err_vs_fp64"] + 1e-8, tag
+
+
+@pytest.mark.parametrize("name", STRICT_CONFIGS)
+def test_strict_parity(name):
+    case = make_case(name, N=4096 if name != "cfg5" else 2048, seed=41)
+    variant = _bound(case)[1].program.kernel_variant
+    _assert_strict(_strict_record(name, gpu_log_prob(case), case, variant))
+
+
+@pytest.mark.parametrize("scheme", ["f16x2", "bf16x3", "fp32"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_trained_weights_parity(name, scheme, monkeypatch):
+    """Weights produced by zenflow_amd.train (tests/golden/make_trained.py) on
+    held-out data, under each kernel scheme: the split schemes scale each
+    layer by one power of two, so trained weight spreads must not cost bits."""
+    from pathlib import Path
+
+    from zenflow_amd.io import load_variables
+
+    if scheme == "fp32":
+        monkeypatch.setenv("ZF_DISABLE_X3", "1")
+    else:
+        monkeypatch.setenv("ZF_X3_SCHEME", scheme)
+    g = Path(__file__).parent / "golden"
+    variables = load_variables(g / f"trained_{name}.npz")
+    d = np.load(g / f"trained_{name}_data.npz")
+    base = make_case(name, N=1, seed=0)
+    case = dict(base, variables=variables, x=d["x"], c=d["c"] if "c" in d.files else None)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == scheme
+    lp = gpu_log_prob(case)
+    check_lp(lp, case, f"trained/{scheme}/{name}")
+    _assert_strict(_strict_record(f"trained_{name}", lp, case, scheme))

@@ -283,10 +283,12 @@ __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, con
       lat = lat + t;
     }
     float lp = lat + ld;
-    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): +-inf -> +-max finite
+    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): JAX's sequential where
+    // chain, each mask taken from the running result — NaN -> -inf ->
+    // finfo.min, +inf -> finfo.max, -inf -> finfo.min.
     if (lp != lp) lp = -INFINITY;
-    else if (lp == INFINITY) lp = 3.40282347e38f;
-    else if (lp == -INFINITY) lp = -3.40282347e38f;
+    if (lp == INFINITY) lp = 3.40282347e38f;
+    if (lp == -INFINITY) lp = -3.40282347e38f;
     if (valid && hh == 0) lp_out[row] = lp;
     if (block_partial != nullptr) {
       double v = (valid && hh == 0) ? (double)lp : 0.0;

@@ -82,8 +82,21 @@ class GlooCommunicator:
 
 
 def nll_from_sum(total_sum: float, n_total: int) -> float:
-    """-mean(log_prob) (train.py:78) from the all-reduced fp64 sum."""
+    """-mean(log_prob) (train.py:78) from the all-reduced fp64 sum.
+
+    The reference's ``jnp.mean`` sums in fp32: a sum outside the fp32 range
+    (two rows at finfo.min after flow.py:47 suffice) makes its NLL infinite,
+    so the fp64 sum keeps that overflow instead of returning a finite mean."""
+    total_sum = float(total_sum)
+    if total_sum != total_sum:
+        return float("nan")
+    if abs(total_sum) >= _F32_MAX_ROUND:  # ties round to even = inf
+        return float("inf") if total_sum < 0 else float("-inf")
     return float(-total_sum / max(1, n_total))
+
+
+# |s| above which fp32 rounding of s gives inf: FLT_MAX + half an ulp (2^103)
+_F32_MAX_ROUND = float(np.finfo(np.float32).max) + 2.0 ** 103
 
 
 class OverlappedAllreduce:

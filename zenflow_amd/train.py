@@ -131,8 +131,10 @@ class Trainer:
 
 def _metric(flow, variables, x, c) -> float:
     """metric_fn (train.py:74-78): -mean(log_prob), eval mode."""
-    lp = flow.apply(variables, x, c)
-    return float(-np.asarray(lp, np.float64).mean())
+    from .dist import nll_from_sum
+
+    lp = np.asarray(flow.apply(variables, x, c), np.float64)
+    return nll_from_sum(lp.sum(), lp.shape[0])
 
 
 def train(
