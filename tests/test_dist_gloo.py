@@ -1,7 +1,8 @@
-"""N>1 data-parallel path on CPU: 2 processes over gloo shard the batch with
-zenflow_amd.dist.shard_rows, evaluate their shard (oracle as the per-rank
-stand-in for the GPU kernel, which needs a GPU) and all-reduce the fp64 NLL
-partial exactly as bench.py does with RCCL.  The global NLL must equal the
+"""N>1 data-parallel path on CPU over gloo (world size 2): the ranks shard
+the batch with zenflow_amd.dist.shard_rows and run dist.DataParallelLogProb
+— the step sequence bench.py runs with RCCL — with the oracle as the per-rank
+stand-in for the GPU kernel (tests/dist_worker.py) and a gloo communicator
+(test-only; the product is torch-free).  The global NLL must equal the
 single-process NLL."""
 
 import os
@@ -24,22 +25,41 @@ def _free_port():
     return p
 
 
+class GlooCommunicator:
+    """fp64 all-reduce through torch.distributed (gloo), with the
+    ``allreduce_sum_`` interface of dist.RcclCommunicator (test-only)."""
+
+    def __init__(self):
+        import torch.distributed as td
+
+        self.td = td
+        self.rank, self.world = td.get_rank(), td.get_world_size()
+
+    def allreduce_sum_(self, buf, stream=None):
+        import torch
+
+        t = torch.from_numpy(np.ascontiguousarray(buf, np.float64))
+        self.td.all_reduce(t)
+        buf[...] = t.numpy()
+        return buf
+
+
 def _worker(rank, world, port, q):
     sys.path.insert(0, str(ROOT))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as td
 
-    from oracle import zf_oracle as O
+    from tests.dist_worker import OracleLogProbStep
     from tests.flowcases import make_case
-    from zenflow_amd.dist import GlooCommunicator, nll_from_sum, shard_rows
+    from zenflow_amd.dist import DataParallelLogProb, shard_rows
 
     td.init_process_group("gloo", rank=rank, world_size=world)
     case = make_case("cfg2", N=1001, seed=5)
     a, b = shard_rows(1001, rank, world)
-    lp, _ = O.flow_log_prob(case["model"], case["variables"], case["x"][a:b], None)
-    comm = GlooCommunicator()
-    total = comm.allreduce_sum_host(np.array([lp.astype(np.float64).sum()]))
-    q.put((rank, b - a, nll_from_sum(float(total[0]), 1001)))
+    dp = DataParallelLogProb(OracleLogProbStep(case), GlooCommunicator(), overlap=False)
+    out = np.empty(b - a, np.float32)
+    dp.step(case["x"][a:b], None, out)
+    q.put((rank, b - a, dp.nll(1001)))
     td.barrier()
     td.destroy_process_group()
 

@@ -1,0 +1,95 @@
+"""The N>1 control plane without torch (zenflow_amd.launch) and the
+data-parallel step sequence (zenflow_amd.dist.DataParallelLogProb) on CPU:
+ranks started by launch.spawn and by a torchrun-style env (no
+ZF_RDZV_DIR), exchanging through the file rendezvous; and bench.py
+--gpus 2 spawning its own ranks."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+WORKER = str(ROOT / "tests" / "dist_worker.py")
+
+
+def _results(d, world):
+    return [json.loads((Path(d) / f"rank{r}.json").read_text()) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spawn_rendezvous_primitives(tmp_path, world):
+    from zenflow_amd.launch import spawn
+
+    assert spawn(world, [WORKER, "prims", str(tmp_path)], timeout=120) == 0
+    res = _results(tmp_path, world)
+    for r in res:
+        assert r["world"] == world
+        assert r["gather"] == [{"r": k, "sq": k * k} for k in range(world)]
+        assert r["bcast"] == "uid-7"
+        assert r["max"] == 1.5 * (world - 1)
+        assert r["sum"] == res[0]["sum"]  # same bits on every rank (rank-order sum)
+    assert len({r["dir"] for r in res}) == 1
+    assert not Path(res[0]["dir"]).exists()  # spawn removed its rendezvous directory
+
+
+def test_spawn_reports_failing_rank(tmp_path):
+    from zenflow_amd.launch import spawn
+
+    code = "import os,sys; sys.exit(3 if os.environ['RANK']=='1' else 0)"
+    assert spawn(2, ["-c", code], timeout=60) == 3
+
+
+def test_two_rank_nll_step(tmp_path):
+    """DataParallelLogProb over 2 spawned ranks (host backend + host
+    communicator) = the single-process NLL over the whole batch."""
+    from oracle import zf_oracle as O
+    from tests.flowcases import make_case
+    from zenflow_amd.launch import spawn
+
+    assert spawn(2, [WORKER, "nll", str(tmp_path)], timeout=180) == 0
+    res = _results(tmp_path, 2)
+    case = make_case("cfg2", N=1001, seed=5)
+    lp, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], None)
+    assert sum(r["rows"] for r in res) == 1001
+    assert np.array_equal(np.concatenate([np.asarray(r["lp"], np.float32) for r in res]), lp)
+    assert res[0]["nll"] == res[1]["nll"]
+    assert res[0]["nll"] == pytest.approx(O.nll(lp), rel=1e-12)
+
+
+def test_torchrun_style_env(tmp_path):
+    """Ranks launched with RANK/WORLD_SIZE/MASTER_PORT only (as
+    torch.distributed.run does, one parent) derive one shared directory."""
+    env = {k: v for k, v in os.environ.items() if k != "ZF_RDZV_DIR"}
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                 MASTER_PORT="29517")
+        procs.append(subprocess.Popen([sys.executable, WORKER, "prims", str(tmp_path)], env=e))
+    assert [p.wait(timeout=120) for p in procs] == [0, 0]
+    res = _results(tmp_path, 2)
+    assert res[0]["dir"] == res[1]["dir"] and "29517" in res[0]["dir"]
+    assert res[1]["bcast"] == "uid-7"
+    assert not Path(res[0]["dir"]).exists()  # rank 0 cleaned up
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two ranks itself;
+    on this GPU-less host each reaches the no-device error of the product
+    path (no CPU fallback)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ZF_RDZV_DIR")}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert p.stderr.count("no HIP device is visible") == 2, p.stderr[-2000:]
+
+
+def test_bench_rejects_mismatched_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr

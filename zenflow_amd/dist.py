@@ -4,8 +4,11 @@ shards, and a single all-reduce of the fp64 NLL partial sum.
 log_prob is a per-sample map in eval mode (BatchNorm running stats,
 ShiftBounds stored min/max), so the only exchange is the scalar
 ``-mean(log_prob)`` of train.py:75-78.  On GPUs it goes through RCCL over
-xGMI (``RcclCommunicator``, librccl via the C ABI); the CPU test suite drives
-the same code with a gloo communicator."""
+xGMI (``RcclCommunicator``, librccl via the C ABI).  No torch: ranks are
+started by ``launch.spawn`` (or torch.distributed.run, the driver's
+launcher) and exchange the RCCL unique id, barriers and timings through
+``launch.FileRendezvous``.  The CPU test suite drives the same step sequence
+(``DataParallelLogProb``) with a host backend and ``HostCommunicator``."""
 
 from __future__ import annotations
 
@@ -31,7 +34,9 @@ class RcclCommunicator:
     """RCCL communicator of one rank (ncclCommInitRank).  ``broadcast`` sends
     the 128-byte unique id from rank 0 to all ranks (any control plane)."""
 
-    def __init__(self, rank: int, world: int, broadcast: Callable[[Optional[bytes]], bytes]):
+    def __init__(self, rank: int, world: int, broadcast: Callable[[Optional[bytes]], bytes],
+                 force: bool = False):
+        self.force = force  # keep a 1-rank communicator in DataParallelLogProb (plumbing checks)
         lib = L.load_library()
         L.ensure_device()
         if not lib.zf_rccl_available():
@@ -63,22 +68,27 @@ class RcclCommunicator:
             self.comm = None
 
 
-class GlooCommunicator:
-    """Host-side fp64 all-reduce through torch.distributed (gloo) — used by
-    the multi-process CPU tests; same interface as RcclCommunicator."""
+class HostCommunicator:
+    """Host-side fp64 all-reduce over the control-plane rendezvous
+    (``launch.FileRendezvous``): the same ``allreduce_sum_`` interface as
+    ``RcclCommunicator`` on numpy buffers, summed in rank order so every rank
+    gets the same bits.  Used where there is no GPU (the multi-process CPU
+    tests) — the GPU data path uses RCCL."""
 
-    def __init__(self):
-        import torch.distributed as td
+    def __init__(self, rdzv):
+        self.rdzv = rdzv
+        self.rank, self.world = rdzv.rank, rdzv.world
 
-        self.td = td
-        self.rank, self.world = td.get_rank(), td.get_world_size()
+    def allreduce_sum_(self, buf: np.ndarray, stream=None) -> np.ndarray:
+        vals = self.rdzv.allgather([float(v) for v in np.asarray(buf, np.float64).ravel()], "allreduce")
+        acc = np.zeros(np.asarray(buf).size, np.float64)
+        for v in vals:
+            acc = acc + np.asarray(v, np.float64)
+        buf[...] = acc.reshape(np.shape(buf))
+        return buf
 
-    def allreduce_sum_host(self, v: np.ndarray) -> np.ndarray:
-        import torch
-
-        t = torch.from_numpy(np.ascontiguousarray(v, np.float64))
-        self.td.all_reduce(t)
-        return t.numpy()
+    def close(self):
+        pass
 
 
 def nll_from_sum(total_sum: float, n_total: int) -> float:
@@ -141,19 +151,74 @@ class OverlappedAllreduce:
         self.i += 1
 
 
-class ShardedLogProb:
-    """log_prob over this rank's shard + global NLL (RCCL all-reduce)."""
+class DeviceLogProbStep:
+    """The product backend of a data-parallel log_prob step on this rank's
+    GPU: the fused kernel over the resident shard (ShiftBounds -> couplings
+    -> latent -> flow.py:47 -> per-block fp64 partials) and the fixed-order
+    NLL reduce of those partials, both on the library stream."""
 
-    def __init__(self, bound_flow, comm: Optional[RcclCommunicator]):
-        self.bf = bound_flow
-        self.comm = comm
-        self.nll = DeviceArray((1,), np.float64)
+    def __init__(self, program, n_rows: int):
+        self.lib = L.load_library()
+        self.program = program
+        self.n_rows = int(n_rows)
+        self.ws = program.workspace(self.n_rows)
 
-    def __call__(self, x_shard: DeviceArray, c_shard=None, out=None) -> DeviceArray:
-        lp = self.bf.log_prob(x_shard, c_shard, out=out, nll_sum=self.nll)
-        if self.comm is not None and self.comm.world > 1:
-            self.comm.allreduce_sum_(self.nll)
-        return lp
+    def new_partial(self) -> DeviceArray:
+        return DeviceArray((1,), np.float64)
 
-    def nll_value(self, n_total: int) -> float:
-        return nll_from_sum(float(self.nll.numpy()[0]), n_total)
+    def kernel(self, x: DeviceArray, c, out: DeviceArray) -> None:
+        p = self.program
+        check(self.lib.zf_flow_log_prob_segment(p.handle, 0, len(p.ops), x.ptr, p._c_ptr(c), None, out.ptr,
+                                                None, self.ws.ptr, self.n_rows, L.stream()), "log_prob")
+
+    def reduce(self, partial: DeviceArray) -> None:
+        check(self.lib.zf_flow_nll_reduce(self.ws.ptr, self.n_rows, partial.ptr, L.stream()), "nll_reduce")
+
+    def read(self, partial: DeviceArray) -> float:
+        return float(partial.numpy()[0])
+
+
+class DataParallelLogProb:
+    """One rank's step of the data-parallel log_prob: the
+    backend's kernel over this rank's shard, its fp64 partial sum of
+    log_prob, and the all-reduce of that partial — overlapped on a
+    communication stream (``OverlappedAllreduce``, device backends) or in
+    order after the reduce.  ``nll(n_total)`` is train.py:78's -mean over the
+    global batch.  bench.py drives the device backend with RCCL; the CPU
+    tests drive this same sequence with a host backend and
+    ``HostCommunicator``."""
+
+    def __init__(self, backend, comm=None, overlap: bool = True, depth: int = 64):
+        self.backend = backend
+        self.comm = comm if comm is not None and comm.world > 1 or _force(comm) else None
+        self.ar = (OverlappedAllreduce(self.comm, depth=depth)
+                   if self.comm is not None and overlap else None)
+        self.partial = backend.new_partial()
+        self.last = None
+
+    def step(self, x, c, out, ev=None) -> None:
+        if ev is not None:
+            ev[0].record()
+        self.backend.kernel(x, c, out)
+        if ev is not None:
+            ev[1].record()
+        if self.ar is not None:
+            buf = self.ar.buffer()
+            self.backend.reduce(buf)
+            self.ar.launch()
+            self.last = buf
+        else:
+            self.backend.reduce(self.partial)
+            if self.comm is not None:
+                self.comm.allreduce_sum_(self.partial)
+            self.last = self.partial
+
+    def nll(self, n_total: int) -> float:
+        if self.last is None:
+            raise RuntimeError("no step has run")
+        return nll_from_sum(self.backend.read(self.last), n_total)
+
+
+def _force(comm) -> bool:
+    """A 1-rank communicator is kept only when asked for (plumbing checks)."""
+    return comm is not None and getattr(comm, "force", False)
