@@ -258,3 +258,32 @@ def test_Flow_two_moons_sample_roundtrip():
     assert xs.shape == (512, 2) and np.isfinite(xs).all()
     lp = flow.apply(case["variables"], xs)
     assert np.isfinite(lp).mean() > 0.95
+
+
+def test_apply_caches_program_by_content():
+    """flow.apply(variables, x) packs and uploads the weights once per
+    distinct variables content (ADVICE r01): same tree -> same program;
+    an in-place change of a leaf -> a new program with the new weights;
+    train-mode calls never reuse (or dirty) the cached eval program."""
+    from tests.flowcases import build_flow, make_case
+
+    case = make_case("cfg1", N=512, seed=43)
+    flow = build_flow(case["cfg"])
+    v = case["variables"]
+    lp1 = flow.apply(v, case["x"])
+    progs = list(flow._programs.values())
+    lp2 = flow.apply(v, case["x"])
+    assert list(flow._programs.values()) == progs and len(progs) == 1
+    assert np.array_equal(lp1, lp2, equal_nan=True)
+    flow.apply(v, case["x"], train=True, mutable=["batch_stats"])
+    assert list(flow._programs.values()) == progs
+    assert np.array_equal(flow.apply(v, case["x"]), lp1, equal_nan=True)
+    # in-place edit of one bias: the digest changes, the output follows the oracle
+    bias = v["params"]["bijector"]["bijectors_1"]["Dense_0"]["bias"]
+    bias += np.float32(0.25)
+    lp3 = flow.apply(v, case["x"])
+    assert len(flow._programs) == 2
+    ref, _ = O.flow_log_prob(case["model"], v, case["x"], None)
+    f = np.isfinite(ref)
+    assert_allclose(lp3[f], ref[f], rtol=2e-5, atol=2e-5)
+    assert not np.allclose(lp3[f], lp1[f])

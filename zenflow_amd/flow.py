@@ -2,9 +2,11 @@
 
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Any, Dict, Optional, Union
 
 import numpy as np
+import xxhash
 
 from . import _lib as L
 from .bijectors import Bijector, Chain, _has_stats, _prep_c
@@ -34,7 +36,7 @@ class Flow(Module):
         cd, _ = _prep_c(c)
         if self.latent._dim is None:
             self.latent._dim = xd.shape[1]
-        prog = self._program(scope.variables, xd.shape[1], 0 if cd is None else cd.shape[1])
+        prog = self._program(scope.variables, xd.shape[1], 0 if cd is None else cd.shape[1], cached=not train)
         if train:
             update = "batch_stats" in scope.mutable
             if not update and _has_stats(self.bijector):
@@ -94,9 +96,30 @@ class Flow(Module):
         return results
 
     # -- helpers ----------------------------------------------------------------
-    def _program(self, variables, D, C) -> Program:
+    _CACHE_SIZE = 4
+
+    def _program(self, variables, D, C, cached: bool = True) -> Program:
+        """The device program for these variables.  Eval-mode programs are
+        cached per (content digest of the variables, D, C, latent), so repeated
+        ``apply(variables, x)`` calls pack and upload the weights once; a
+        digest (xxh3 over every leaf's bytes, ~0.1 ms/MB) rather than object
+        identity, because numpy leaves can be changed in place.  Train-mode
+        calls write batch statistics into their program and never share it."""
         sub = {k: (v or {}).get("bijector", {}) for k, v in (variables or {}).items()}
-        return Program(self.bijector, sub, D, C, latent=self.latent)
+        if not cached:
+            return Program(self.bijector, sub, D, C, latent=self.latent)
+        key = (_digest(sub), int(D), int(C), type(self.latent).__name__,
+               getattr(self.latent, "peakness", None), self.latent._dim)
+        cache = self.__dict__.setdefault("_programs", OrderedDict())
+        prog = cache.get(key)
+        if prog is None:
+            prog = Program(self.bijector, sub, D, C, latent=self.latent)
+            cache[key] = prog
+            while len(cache) > self._CACHE_SIZE:
+                cache.popitem(last=False)
+        else:
+            cache.move_to_end(key)
+        return prog
 
     def _init_variables(self, gen, D, C, params, stats):
         p: Dict = {}
@@ -116,6 +139,23 @@ class Flow(Module):
         if self.latent._dim is None:
             self.latent._dim = dim
         return BoundFlow(self._program(variables, dim, cond_dim))
+
+
+def _digest(tree) -> str:
+    """Content digest of a variables tree: paths, shapes, dtypes and bytes."""
+    h = xxhash.xxh3_128()
+
+    def walk(node, path):
+        if isinstance(node, dict):
+            for k in sorted(node):
+                walk(node[k], path + "/" + str(k))
+            return
+        a = np.ascontiguousarray(np.asarray(node))
+        h.update(f"{path}:{a.dtype.str}:{a.shape};".encode())
+        h.update(memoryview(a).cast("B"))
+
+    walk(tree, "")
+    return h.hexdigest()
 
 
 class BoundFlow:

@@ -27,13 +27,17 @@ from pathlib import Path
 from typing import Any, List, Optional, Sequence
 
 
-def spawn(n: int, argv: Sequence[str], env: Optional[dict] = None, timeout: Optional[float] = None) -> int:
+def spawn(n: int, argv: Sequence[str], env: Optional[dict] = None, timeout: Optional[float] = None,
+          grace: float = 20.0) -> int:
     """Run ``python argv`` as ranks 0..n-1 (one process per GPU) and wait.
 
     Returns 0 if every rank exited 0, else the first non-zero status (a
     negative signal number is mapped to 128 + signal, as a shell would).
-    The parent never initialises the GPU, so exec-free process creation is
-    safe on this pool."""
+    When one rank fails, the others get ``grace`` seconds to end on their
+    own (and report their own error) before they are terminated: a rank
+    blocked in the rendezvous on the failed one would otherwise wait out
+    its timeout.  The parent never initialises the GPU, so exec-free
+    process creation is safe on this pool."""
     if n < 1:
         raise ValueError("n must be >= 1")
     rdzv = tempfile.mkdtemp(prefix="zf_rdzv_")
@@ -55,8 +59,11 @@ def spawn(n: int, argv: Sequence[str], env: Optional[dict] = None, timeout: Opti
             if s != 0 and rc == 0:
                 rc = s if s > 0 else 128 - s
             if s != 0:  # one rank failed: the others would wait for it forever
+                until = time.monotonic() + grace
                 for q in procs:
-                    if q.poll() is None:
+                    try:
+                        q.wait(timeout=max(0.0, until - time.monotonic()))
+                    except subprocess.TimeoutExpired:
                         q.terminate()
         for p in procs:
             try:
