@@ -48,6 +48,10 @@ WORKLOADS = {
     "cfg3s": (4, 0, 16, (128, 128), 4, "normal", "sample"),  # Flow.sample, latent drawn on device
     "cfg4": (2, 2, 16, (128, 128), 2, "beta", "log_prob"),
     "cfg5": (16, 0, 32, (256, 256), 8, "normal", "log_prob"),
+    # reference defaults at dim 8 (rolling_spline_coupling(8): 8 couplings,
+    # knots 16, layers (128, 128)), and K = 32 at hidden 128
+    "d8": (8, 0, 16, (128, 128), 8, "normal", "log_prob"),
+    "d4k32": (4, 0, 32, (128, 128), 4, "normal", "log_prob"),
 }
 
 

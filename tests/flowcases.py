@@ -25,6 +25,17 @@ CONFIGS = {
     # hidden 128 with dc = 2 and a condition; hidden 256 (dim-pair path)
     "d3c1": dict(D=3, C=1, K=16, layers=(128, 128), latent="normal"),
     "d2h256": dict(D=2, C=0, K=32, layers=(256, 256), latent="normal"),
+    # the reference defaults rolling_spline_coupling(dim, knots=16, layers=(128, 128))
+    # at dim >= 6 (dim-pair loop at hidden 128), K = 32 at hidden 128, K = 8 at
+    # hidden 256, hidden 64 (padded to 128 on the split-MFMA kernel)
+    "d6": dict(D=6, C=0, K=16, layers=(128, 128), latent="normal"),
+    "d8": dict(D=8, C=0, K=16, layers=(128, 128), latent="normal"),
+    "d16": dict(D=16, C=0, K=16, layers=(128, 128), latent="normal"),
+    "d7k32c2": dict(D=7, C=2, K=32, layers=(128, 128), latent="truncated_normal", couplings=4),
+    "d4k32": dict(D=4, C=0, K=32, layers=(128, 128), latent="normal"),
+    "d3k32": dict(D=3, C=0, K=32, layers=(128, 96), latent="beta"),
+    "d4h256k8": dict(D=4, C=1, K=8, layers=(256, 256), latent="normal"),
+    "d5h64": dict(D=5, C=0, K=16, layers=(64, 64), latent="normal"),
 }
 
 

@@ -71,7 +71,11 @@ def check_lp(lp, case, tag=""):
     return err.max()
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"])
+WIDE_SHAPES = ["d6", "d8", "d16", "d7k32c2", "d4k32", "d3k32", "d4h256k8", "d5h64"]
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"]
+                         + WIDE_SHAPES)
 @pytest.mark.parametrize("N", [1, 1000, 4096])
 def test_log_prob_parity(name, N):
     case = make_case(name, N=N, seed=11)
@@ -83,7 +87,7 @@ def test_log_prob_parity_cfg5():
     check_lp(gpu_log_prob(case), case, "cfg5")
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES)
 def test_inverse_parity(name):
     case = make_case(name, N=2000, seed=13)
     rng = np.random.default_rng(7)
@@ -99,7 +103,7 @@ def test_inverse_parity(name):
     assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
 
 
-@pytest.mark.parametrize("name", ["cfg2", "odd", "cfg4", "d3c1", "d2h256"])
+@pytest.mark.parametrize("name", ["cfg2", "odd", "cfg4", "d3c1", "d2h256", "d8", "d7k32c2", "d4h256k8"])
 def test_chain_forward_parity(name):
     """Chain.__call__ (y, log_det) vs the oracle's chain."""
     case = make_case(name, N=3000, seed=14)
@@ -257,13 +261,12 @@ def test_golden_edges(name):
 
 
 # --- kernel variants -----------------------------------------------------------
-# Shapes the split-MFMA kernel takes (hidden <= 128 with knots 8/16 and dim <= 5;
-# hidden 256 with knots 16/32 and dim <= 17) run on it by default, in the f16x2
-# scheme; ZF_X3_SCHEME=bf16x3 selects the three-term bf16 scheme and
-# ZF_DISABLE_X3=1 the fp32-MFMA kernel, which must stay parity-green on the
-# same shapes.
+# Shapes the split-MFMA kernel takes (hidden <= 256, one knot count in
+# {8, 16, 32}, dim <= 64) run on it by default, in the f16x2 scheme;
+# ZF_X3_SCHEME=bf16x3 selects the three-term bf16 scheme and ZF_DISABLE_X3=1
+# the fp32-MFMA kernel, which must stay parity-green on the same shapes.
 
-X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"]
+X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"])

@@ -478,6 +478,10 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   F.latent = desc.latent;
   F.n_ops = desc.n_ops;
   F.HP = zf::hidden_pad_of(&desc);
+  int x3K = 0;
+  // the split-MFMA kernel runs hidden <= 128 padded to 128 (4 tiles)
+  const bool x3 = zf::x3_eligible(desc, F.HP < 128 ? 128 : F.HP, &x3K);
+  if (x3 && F.HP < 128) F.HP = 128;
   const int HP = F.HP, T = HP / 32;
   // Latent constants in fp32, as jax.scipy.stats computes them.
   {
@@ -499,8 +503,6 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   int64_t off = 0;
   auto take = [&](int64_t n) { const int64_t o = off; off = zf::round_up64(off + n, 4); return o; };
   int nslot = 1;
-  int x3K = 0;
-  const bool x3 = zf::x3_eligible(desc, HP, &x3K);
   // Small per-op parameters (ShiftBounds rows, BatchNorm, first Dense,
   // biases) first, for all ops: the bf16x3 kernel stages [0, small_floats)
   // in LDS once per block.  The streamed fp32 weight fragments follow.
@@ -595,7 +597,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   }
   std::vector<uint16_t> x3s;
   const int NT = zf::x3_scheme();
-  if (x3 && zf::x3_lds_bytes(T, desc.dim, NT) <= 160 * 1024) {
+  if (x3 && zf::x3_lds_bytes(zf::x3_buf_tiles(desc, T, x3K), desc.dim, NT) <= 160 * 1024) {
     zf::x3_pack(desc, nat, T, NT, F, P, x3s);
     F.x3_ok = NT == 3 ? 1 : 2;
     h->x3_K = x3K;

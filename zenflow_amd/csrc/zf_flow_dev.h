@@ -335,7 +335,8 @@ int launch_flow_x3(const X3Launch& a, bool inverse);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
 int x3_pairs(const zf_flow_desc& desc);
-size_t x3_lds_bytes(int T, int D, int NT);
+int x3_buf_tiles(const zf_flow_desc& desc, int T, int K);
+size_t x3_lds_bytes(int TB, int D, int NT);
 int x3_scheme();
 void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);

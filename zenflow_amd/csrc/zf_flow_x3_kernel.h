@@ -1,0 +1,856 @@
+// Split-MFMA fused flow kernel (K3): the whole op chain of
+// flow_kernel (zf_flow.hip) in one launch, with the conditioner's streamed
+// Dense layers (hidden -> hidden and hidden -> spline parameters) on 16-bit
+// MFMA using a split of both fp32 operands:
+//   * f16x2 (default): x*2^k = hi + lo, two RNE fp16 terms of power-of-two
+//     scaled operands, three v_mfma_f32_32x32x16_f16 products per k-step
+//     (lo*hi + hi*lo + hi*hi), fp32 accumulate;
+//   * bf16x3 (ZF_X3_SCHEME=bf16x3): x = hi + mid + lo, three RNE bf16 terms,
+//     six v_mfma_f32_32x32x16_bf16 products per k-step, small terms first —
+//     an fp32 dot product to ~1e-7 relative (tests/hip/mfma_bf16x3_layout.hip).
+//
+// Execution model:
+//   * 4 waves x 32 samples = 128 samples per block; hidden 128 (T = 4): 3
+//     blocks per CU (168 VGPRs), or 2 with a dim-pair loop / K = 32;
+//     hidden 256 (T = 8): one block per CU (the 8 + 8 accumulator tiles take
+//     a wave's whole VGPR + AGPR file).
+//   * Weights are the MFMA A operand, pre-split on the host and packed in the
+//     exact per-lane fragment order; each streamed layer is a sequence of
+//     "groups" (one 32-row input tile x all output tiles x terms: 16 KiB for
+//     128 -> 128 at f16x2) that the block DMAs global -> LDS
+//     (global_load_lds_dwordx4, no VGPR staging) one group ahead into a
+//     double buffer, so a weight byte crosses L2 -> CU once per block.
+//   * The B operand is the previous layer's fp32 accumulator tile, split in
+//     registers (accumulator-as-operand: k-step s of a tile uses accumulator
+//     registers 8s..8s+7; A is packed with the same k order, no shuffles).
+//   * The last layer's rows are permuted so that lane half h of every output
+//     tile holds 16 consecutive spline parameters of transformed dim h
+//     (ONE, dim 2-3: 32 parameters of the one dim per tile): the whole
+//     normalize_spline_params + bin search + RQ spline runs from registers;
+//     more than 2 transformed dims loop over dim pairs (PAIRS).
+//   * Layer 0 (BatchNorm'd conditioning inputs, 1-2 k-steps, fp32 MFMA),
+//     ShiftBounds, Roll and the latent epilogue are shared with flow_kernel
+//     (zf_flow_dev.h).
+// Eligibility (host, x3_eligible): hidden widths <= 256 (<= 128 padded to
+// 128), one knot count in {8, 16, 32} for all couplings, dim <= 64.
+// Everything else, and ZF_DISABLE_X3=1, runs flow_kernel.
+#pragma once
+#include "zf_flow_dev.h"
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace zf {
+namespace {
+
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+// Split scheme (NT = terms per operand):
+//   NT = 3 "bf16x3": x = hi + mid + lo (RNE bf16 each), six products per
+//          k-step — an fp32 dot product to ~1e-7 relative;
+//   NT = 2 "f16x2":  x*2^k = hi + lo (RNE fp16 each; 11-bit significands, so
+//          the pair holds 22 bits) with hi*hi + hi*lo + lo*hi — three
+//          products, each within ~2^-22 relative.  Operands are scaled by
+//          powers of two into fp16's range: weights per layer on the host
+//          (max |W| * 2^kw in [2^13, 2^14)), activations per sample in the
+//          kernel (x3_act_scale); the accumulator is scaled back exactly.
+template <int NT>
+struct XT;
+template <>
+struct XT<3> {
+  using E = bf16x8;
+  static constexpr int kProd = 6;
+};
+template <>
+struct XT<2> {
+  using E = halfx8;
+  static constexpr int kProd = 3;
+};
+
+// Hidden 256 (one wave per SIMD, nothing else to hide LDS latency or fill
+// MFMA issue gaps): A fragments one output tile ahead, and each group's
+// MFMAs interleaved with its VALU by sched_group_barrier (measured +4-5% at
+// cfg5; at T = 4 both were neutral to -12% and stay off).
+#ifndef ZF_X3_WIDE_SCHED
+#define ZF_X3_WIDE_SCHED 3
+#endif
+
+// f16x2, hidden <= 128: seed the accumulators with bias / us (1) instead of
+// joining the bias at the layer's end with one fma (0).
+#ifndef ZF_X3_SEED_SCALED
+#define ZF_X3_SEED_SCALED 1
+#endif
+
+
+constexpr int kX3Waves = 4;  // waves per block: 128 samples
+// Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
+template <int NT>
+constexpr int group_bytes(int NOUT) { return 2 * NOUT * NT * 1024; }
+
+
+// Regs 8s..8s+7 of an accumulator tile -> hi / mid / lo bf16x8 (RNE each).
+template <int S>
+__device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm, bf16x8& bl) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx2 x = {v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
+    const bf16x2 h = __builtin_convertvector(x, bf16x2);
+    const floatx2 r = x - __builtin_convertvector(h, floatx2);
+    const bf16x2 m = __builtin_convertvector(r, bf16x2);
+    const floatx2 r2 = r - __builtin_convertvector(m, floatx2);
+    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
+    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
+    bm[2 * i] = m[0]; bm[2 * i + 1] = m[1];
+    bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
+  }
+}
+
+// Regs 8s..8s+7 of an (already scaled) activation tile -> hi / lo fp16x8
+// (RNE each; the residual x - hi is exact).  ZF_X3_MIXSPLIT: the lo term by
+// v_fma_mix{lo,hi}_f16 (x*1 - f32(hi) rounded to f16 in one instruction:
+// 3 instead of 5 VALU per value pair, bit-identical —
+// tests/hip/f16_split_mix.hip).
+#ifndef ZF_X3_MIXSPLIT
+#define ZF_X3_MIXSPLIT 1
+#endif
+template <int S>
+__device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& bl) {
+#if ZF_X3_MIXSPLIT
+  // One asm statement for all eight lo terms, ending in `s_nop 1`: hipcc
+  // pads no hazard inside or after an asm statement, and its outputs feed an
+  // MFMA operand, which needs two wait states after a VALU write (without
+  // the pad a schedule that put the MFMA right behind the asm read stale
+  // operands).
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const halfx2 hv = __builtin_convertvector(floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]}, halfx2);
+    __builtin_memcpy(&h[i], &hv, 4);
+  }
+  asm(
+      "v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, 1.0, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, 1.0, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, 1.0, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, 1.0, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(l[0]), "=&v"(l[1]), "=&v"(l[2]), "=&v"(l[3])
+      : "v"(v[8 * S + 0]), "v"(v[8 * S + 1]), "v"(v[8 * S + 2]), "v"(v[8 * S + 3]), "v"(v[8 * S + 4]),
+        "v"(v[8 * S + 5]), "v"(v[8 * S + 6]), "v"(v[8 * S + 7]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
+  __builtin_memcpy(&bh, h, 16);
+  __builtin_memcpy(&bl, l, 16);
+#else
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
+    const halfx2 h = __builtin_convertvector(x, halfx2);
+    const floatx2 r = x - __builtin_convertvector(h, floatx2);
+    const halfx2 l = __builtin_convertvector(r, halfx2);
+    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
+    bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
+  }
+#endif
+}
+
+template <int NT, int S>
+__device__ __forceinline__ void splitk(const floatx16& v, typename XT<NT>::E (&b)[NT]) {
+  if constexpr (NT == 3) {
+    split8<S>(v, b[0], b[1], b[2]);
+  } else {
+    split8h<S>(v, b[0], b[1]);
+  }
+}
+
+// f16x2: every swished layer (Dense_0 .. Dense_{n_hidden-1}) is packed with
+// its weights and bias multiplied by log2(e) (x3_pack), so its accumulator
+// holds v' = v*log2(e) and the sigmoid's exponent needs no multiply.
+constexpr float kSwishPrescale = 1.44269504088896341f;
+
+// Layer-input activation: swish(v) (bf16x3), or f16x2's swish(v) * sc from
+// the prescaled v' with c = isc*log2(e) (isc = 1/sc a power of two):
+//   swish(v) * sc = v' / ((1 + 2^-v') * c)  — one fma, exp2, rcp, mul, so
+// neither the exponent scale nor the activation scale costs an instruction.
+template <int NT>
+__device__ __forceinline__ float act_swish(float v, float c) {
+#if ZF_SWISH_MODE == 0
+  if constexpr (NT == 2) {
+    const float e = __builtin_amdgcn_exp2f(-v);
+    return v * __builtin_amdgcn_rcpf(__builtin_fmaf(e, c, c));
+  }
+  return swish(v);
+#else
+  if constexpr (NT == 2) return swish(v * (1.0f / kSwishPrescale)) * (kSwishPrescale / c);
+  return swish(v);
+#endif
+}
+
+__device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                          const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
+                                          floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// One k-step of the split product, small terms first.
+template <int NT>
+__device__ __forceinline__ floatx16 mfma_split(const typename XT<NT>::E (&a)[NT], const typename XT<NT>::E (&b)[NT],
+                                               floatx16 acc) {
+  if constexpr (NT == 3) {
+    return mfma3(a[0], a[1], a[2], b[0], b[1], b[2], acc);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
+  }
+}
+
+// A fragment (NT parts of 1 KiB; this lane's 16 bytes of each) from LDS.
+template <int NT>
+__device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)[NT]) {
+  using E = typename XT<NT>::E;
+  if constexpr (NT == 3) f[1] = *reinterpret_cast<const E*>(a + 1024);
+  f[0] = *reinterpret_cast<const E*>(a);
+  if constexpr (NT == 3) f[2] = *reinterpret_cast<const E*>(a + 2048);
+  else f[1] = *reinterpret_cast<const E*>(a + 1024);
+}
+
+// f16x2: per-sample power-of-two scale sc = 1/isc of a layer input, from its
+// raw (log2(e)-prescaled) pre-activations, so its largest |swish| lands below
+// 2^14 (|swish(v)| <= |v| < |v'|), and the exact factor that undoes both
+// scales on the accumulator: us = 2^-(e_act + kw) (ius = 1/us).  Returned
+// in isc: the swish constant c = isc*log2(e) (act_swish).  Lanes l and l^32
+// hold the same sample.
+template <int T>
+__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius) {
+  float m = 0.f;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
+  // seeded as bias / us stays finite)
+  const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
+  isc = __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
+  us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
+  ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
+}
+
+// Layer end: acc = acc * us + bias (f16x2: undo the scales) or acc + bias.
+template <int NT>
+__device__ __forceinline__ floatx16 x3_finish(const floatx16& acc, float us, const floatx16& b) {
+  if constexpr (NT == 2) {
+    floatx16 r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = __builtin_fmaf(acc[i], us, b[i]);
+    return r;
+  } else {
+    return acc + b;
+  }
+}
+
+// One weight group from LDS: input tile Q (2 k-steps of 16) into NOUT
+// output tiles.  Block (s, o, part) is 1 KiB at ((s*NOUT + o)*NT + part) KiB;
+// lane l's 16 bytes at l*16.
+template <int NT, int T, int NOUT, int Q>
+__device__ __forceinline__ void x3_group(const char* buf, const floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
+                                         int lane) {
+  using E = typename XT<NT>::E;
+  const char* lb = buf + lane * 16;
+if constexpr (T == 8) {
+  // A fragments one output tile ahead (LDS latency off the MFMA chain).
+  E c[NT];
+  load_frag<NT>(lb, c);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    E b[NT];
+    if (s == 0) splitk<NT, 0>(hb[Q], b);
+    else splitk<NT, 1>(hb[Q], b);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      const int t = s * NOUT + o;
+      E n[NT];
+      if (t + 1 < 2 * NOUT) load_frag<NT>(lb + (((t + 1) * NT) << 10), n);
+      acc[o] = mfma_split<NT>(c, b, acc[o]);
+      if (t + 1 < 2 * NOUT) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) c[i] = n[i];
+      }
+    }
+  }
+} else {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    E b[NT];
+    if (s == 0) splitk<NT, 0>(hb[Q], b);
+    else splitk<NT, 1>(hb[Q], b);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      E a[NT];
+      load_frag<NT>(lb + (((s * NOUT + o) * NT) << 10), a);
+      acc[o] = mfma_split<NT>(a, b, acc[o]);
+    }
+  }
+}
+}
+
+// The group stream of the NSC being computed (byte offsets into the x3
+// blob), set up at NSC entry from the op's scalar fields: the per-step
+// prefetch then needs no memory access of its own (a scalar load there would
+// make its lgkmcnt wait drain the step's LDS reads too).  Groups in order:
+// hidden layers (T groups each), then the last layer (T groups per pair of
+// transformed dims).
+struct X3Span {
+  long long base;       // group 0 of this NSC
+  long long next_base;  // group 0 of the next NSC in execution order within range, or -1
+  int G, nhid;          // groups in this NSC, hidden-layer groups among them
+  int last_pieces;      // KiB pieces of one last-layer group
+  int next_pieces;      // KiB pieces of the next NSC's group 0
+};
+
+template <int NT, int T>
+__device__ __forceinline__ int first_pieces(const DevOp& op) {
+  return (op.n_hidden > 1 ? group_bytes<NT>(T) : group_bytes<NT>(op.x3_tlast)) >> 10;
+}
+
+template <int NT, int T, bool INV>
+__device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int oi, int op_begin, int op_end) {
+  const DevOp& op = F->ops[oi];
+  X3Span sp;
+  sp.base = op.x3;
+  sp.G = op.x3_groups;
+  sp.nhid = T * (op.n_hidden - 1);
+  sp.last_pieces = group_bytes<NT>(op.x3_tlast) >> 10;
+  const int n = op.x3_next[INV ? 1 : 0];
+  if (n >= op_begin && n < op_end) {
+    sp.next_base = F->ops[n].x3;
+    sp.next_pieces = first_pieces<NT, T>(F->ops[n]);
+  } else {
+    sp.next_base = -1;
+    sp.next_pieces = 0;
+  }
+  return sp;
+}
+
+// Issue the DMA of one group into an LDS buffer: 1 KiB pieces (one
+// global_load_lds_dwordx4 per wave: wave-uniform LDS base, lane*16 implied)
+// spread over the block's waves.
+__device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave, int lane) {
+  for (int p = wave; p < pieces; p += kX3Waves)
+    __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
+}
+
+// Block-wide weight-group pipeline state (every field wave-uniform).
+struct X3Pipe {
+  char* cur;    // LDS buffer holding the group this wave computes next
+  char* nxt;    // the other buffer of the double buffer (the prefetch target)
+  int g;        // index of that group within the current NSC
+  X3Span span;  // current NSC's group stream
+  int wave;
+};
+
+// DMA the group after group p.g (the next one of this NSC, or group 0 of
+// the next NSC) into `dst`; nothing at the end of the stream.
+template <int NT, int T>
+__device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
+  constexpr int kHid = group_bytes<NT>(T);
+  const int g = p.g + 1;
+  long long off;
+  int pieces;
+  if (g < p.span.nhid) {
+    off = p.span.base + (long long)g * kHid;
+    pieces = kHid >> 10;
+  } else if (g < p.span.G) {
+    off = p.span.base + (long long)p.span.nhid * kHid + (long long)(g - p.span.nhid) * (p.span.last_pieces << 10);
+    pieces = p.span.last_pieces;
+  } else {
+    if (p.span.next_base < 0) return;
+    off = p.span.next_base;
+    pieces = p.span.next_pieces;
+  }
+  x3_dma(x3 + off, dst, pieces, p.wave, lane);
+}
+
+// One pipeline step: wait for this wave's DMAs, block barrier (the group in
+// buffer `buf` is complete and the other buffer is free), prefetch the next
+// group into it, then this group's MFMAs.  `bias` (optional): bias tiles of
+// a layer whose accumulators did not start from the bias, loaded here — in
+// the layer's last step, when its earlier input tiles are dead — and joined
+// after the MFMAs (x3_finish, which also undoes the f16x2 scales).
+template <int NT, int T, int NOUT, int Q, bool SW>
+__device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                        floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                        int hh, float isc, float us) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+  if (bias != nullptr) {
+    floatx16 bt[NOUT];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+    x3_group<NT, T, NOUT, Q>(p.cur, hb, acc, lane);
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+  } else {
+    x3_group<NT, T, NOUT, Q>(p.cur, hb, acc, lane);
+  }
+  // SW: the layer input arrives as pre-activations except tile 0; the swish
+  // of tile Q+1 goes here, in the same scheduling region as this group's
+  // MFMAs, whose issue gaps it fills.
+  if constexpr (SW && Q + 1 < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+  }
+  if constexpr (T == 8 && ZF_X3_WIDE_SCHED > 0) {
+    // the k-step-0 split first, then every MFMA followed by its share of LDS
+    // reads and VALU (split of k-step 1, the deferred swish)
+    constexpr int kP = XT<NT>::kProd;
+    __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
+    __builtin_amdgcn_sched_group_barrier(0x402, 20, 0);
+#pragma unroll
+    for (int i = 0; i < 2 * kP * NOUT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((NT == 3 && i % 2 == 0) || (NT == 2 && i % 3 != 2)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_WIDE_SCHED, 0);
+    }
+  }
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+
+// k-step-level software pipeline (hidden 128, one pass per layer): group Q
+// multiplies k-step (Q, 0) with the split carried in `cs`, and beside its
+// MFMAs forms the split of (Q, 1), the swish of tile Q+1 and the split of
+// (Q+1, 0) for the next group — so the bf16 split and the deferred swish sit
+// in the MFMA issue gaps of the same wave (cross-wave they would not overlap:
+// tests/hip/coexec_probe.hip modes 2 and 6).
+#ifndef ZF_X3_PIPE
+#define ZF_X3_PIPE 1
+#endif
+template <int NT, int T, int NOUT, int Q, bool HASB>
+__device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                             floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                             int hh, typename XT<NT>::E (&cs)[NT], float isc, float us) {
+  using E = typename XT<NT>::E;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+  floatx16 bt[NOUT];
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+  }
+  const char* lb = p.cur + lane * 16;
+  E s1[NT];
+  splitk<NT, 1>(hb[Q], s1);
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    E a[NT];
+    load_frag<NT>(lb + ((o * NT) << 10), a);
+    acc[o] = mfma_split<NT>(a, cs, acc[o]);
+  }
+  if constexpr (Q + 1 < T) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+    splitk<NT, 0>(hb[Q + 1], cs);
+  }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    E a[NT];
+    load_frag<NT>(lb + (((NOUT + o) * NT) << 10), a);
+    acc[o] = mfma_split<NT>(a, s1, acc[o]);
+  }
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+  }
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+
+// A pipelined layer: hb[0] already swished, cs = split of (0, 0).
+template <int NT, int T, int NOUT, bool HASB, int Q = 0>
+__device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                              floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
+                                              typename XT<NT>::E (&cs)[NT], float isc, float us) {
+  if constexpr (Q + 1 < T) {
+    x3_step_pipe<NT, T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us);
+    x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+  } else {
+    x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+  }
+}
+
+// A whole streamed Dense layer: T groups (one per input tile).
+template <int NT, int T, int NOUT, bool SW, int Q = 0>
+__device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                         floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
+                                         float isc, float us) {
+  if constexpr (Q + 1 < T) {
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh, isc, us);
+    x3_layer<NT, T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
+  } else {
+    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
+  }
+}
+
+// squareplus with a Newton-corrected reciprocal square root (one
+// transcendental instead of sqrt + rcp): ~0.5 ulp, like sqrtf.
+__device__ __forceinline__ float squareplus_rsq(float x) {
+  const float a = x * x + 4.0f;
+  const float r = __builtin_amdgcn_rsqf(a);
+  float sq = a * r;
+  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * r, sq);
+  return 0.5f * (x + sq);
+}
+
+// Spline arithmetic of the split-MFMA kernel (ZF_X3_FASTSPLINE=1): the
+// spline parameters already differ from the reference's in the last ulp
+// (GEMM summation order), so the per-lane spline uses ~1-ulp hardware forms:
+// squareplus from v_sqrt_f32 (no Newton step), quotients from a refined
+// reciprocal, and the log-det as ONE log of the product of its three terms
+// (2 log(sk+eps) + log(num2+eps) - 2 log(den+eps), utils.py:133-135).
+// Parity is checked by the same per-sample tolerance as every other path.
+#ifndef ZF_X3_FASTSPLINE
+#define ZF_X3_FASTSPLINE 1
+#endif
+__device__ __forceinline__ float x3_squareplus(float x) {
+#if ZF_X3_FASTSPLINE
+  return 0.5f * (x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f)));
+#else
+  return squareplus_rsq(x);
+#endif
+}
+
+// 2*squareplus(x): the widths and heights are normalised by their sum, so the
+// factor 1/2 cancels exactly (a power of two): bit-identical knots.
+__device__ __forceinline__ float x3_squareplus2(float x) {
+#if ZF_X3_FASTSPLINE
+  return x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f));
+#else
+  return 2.0f * squareplus_rsq(x);
+#endif
+}
+
+__device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
+#if ZF_X3_FASTSPLINE
+  const float rw = rcp_refined(b.w);
+  const float sk = b.h * rw;
+  const float zr = (x - b.xk) * rw;  // :122
+  const float z = (zr != zr) ? zr : fminf(fmaxf(zr, kEps), kOneMinusEps);
+  const float az = 1.0f - z;
+  const float num = b.h * z * (sk * z + b.dk * az);                // :125
+  const float den = sk + (b.dkp1 + b.dk - 2.0f * sk) * z * az;     // :126
+  const float rd = rcp_refined(den + kEps);
+  const float yv = b.yk + num * rd;                                // :127
+  y = b.oob ? x : yv;                                              // :130
+  const float num2 = z * (b.dkp1 * z + 2.0f * sk * az) + b.dk * (az * az);  // :133
+  const float sq = (sk + kEps) * rd;
+  const float l = __logf((num2 + kEps) * (sq * sq));
+  ld = b.oob ? 0.0f : l;                                           // :138
+#else
+  rqs_forward_eval(x, b, y, ld);
+#endif
+}
+
+// Block: 4 waves x 32 samples, one 32-row input tile per weight group,
+// double-buffered in LDS.  Small parameters (BatchNorm, first Dense, biases,
+// ShiftBounds rows) are read from global memory (L2-resident), so the LDS
+// footprint is 2 groups + the state: 50 KiB at T = 4 (3 blocks = 3 waves per
+// SIMD, <= 168 VGPRs), 104 KiB at T = 8 (hidden 256: one block per CU, the
+// 8 + 8 accumulator tiles need one wave's whole register file).
+// ONE (one transformed dim, dim 2 or 3): the last layer's rows carry that
+// dim's parameters in both lane halves (tile o, half h, register r =
+// parameter 32o + 16h + r), so it takes ceil((3K-1)/32) tiles instead of
+// ceil((3K-1)/16) half-empty ones, and the halves swap theirs by a lane
+// shuffle before the spline.
+#ifndef ZF_X3_NARROW_OCC
+#define ZF_X3_NARROW_OCC 3
+#endif
+// Waves per SIMD: hidden 128 with one dim pair and K <= 16 fits 168 VGPRs (3);
+// a dim-pair loop keeps the hidden activations live across the last layer,
+// and K = 32 holds 95 spline parameters per lane: 256 VGPRs (2); hidden 256
+// needs the whole register file (1).
+template <int T, int K, bool PAIRS>
+constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : ZF_X3_NARROW_OCC; }
+
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV>
+__global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
+    const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
+    const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
+    const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
+    double* __restrict__ block_partial, long long nparts, int op_begin, int op_end, long long N,
+    unsigned long long seed, int gen) {
+  // last-layer tiles per dim pair: 16 parameters per lane half (ONE: 32 of one dim per tile)
+  constexpr int TL = ONE ? (3 * K - 1 + 31) / 32 : (3 * K - 1 + 15) / 16;
+  constexpr int NPV = ONE ? 32 * TL : 16 * TL;  // spline parameters held per lane
+  constexpr int NW = kX3Waves;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int D = F->D;
+  const int C = F->C;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar cursor math
+  const int lane = threadIdx.x & 63;
+  const int s = lane & 31;
+  const int hh = lane >> 5;
+  // one LDS weight buffer holds a hidden-layer group (T output tiles) or a
+  // last-layer group (TL tiles: more than T at K = 32, hidden 128)
+  constexpr int kBuf = group_bytes<NT>(T > TL ? T : TL);
+  // LDS: [2][kBuf] weight groups | [NW][D][32] state | [NW] partials
+  float* xs = reinterpret_cast<float*>(lds + 2 * kBuf) + wave * (32 * D);
+  double* s_part = reinterpret_cast<double*>(reinterpret_cast<float*>(lds + 2 * kBuf) + NW * 32 * D);
+  const float* sp = blob;
+  const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
+  const bool valid = row < N;
+
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
+  float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
+  int rot = 0;
+  wave_lds_sync();
+
+  X3Pipe pipe;
+  pipe.cur = lds;
+  pipe.nxt = lds + kBuf;
+  pipe.g = 0;
+  pipe.wave = wave;
+  {  // group 0 of the first NSC in execution order goes out now
+    int first = -1;
+    const int nq = op_end - op_begin;
+    for (int q = 0; q < nq; ++q) {
+      const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+      if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
+    }
+    if (first >= 0) x3_dma(x3 + F->ops[first].x3, pipe.cur, first_pieces<NT, T>(F->ops[first]), wave, lane);
+  }
+
+  const KnotConsts kc(K);
+  const int nq = op_end - op_begin;
+  for (int q = 0; q < nq; ++q) {
+    const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+    const DevOp& op = F->ops[oi];
+    const int kind = op.kind;
+    if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
+      rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
+    } else if (kind == ZF_OP_SHIFT_BOUNDS) {
+      shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
+    } else {  // ZF_OP_NSC, bijectors.py:329-371
+      pipe.span = make_span<NT, T, INV>(F, oi, op_begin, op_end);
+      pipe.g = 0;
+      floatx16 hb[T];
+      // The swish of a layer's output is deferred tile by tile into the next
+      // streamed layer (x3_step, SW) — except before a PAIRS last layer,
+      // which passes over its input once per dim pair.
+      constexpr bool kLastSW = !PAIRS;
+      constexpr bool kPipe = T == 4 && !PAIRS && ZF_X3_PIPE;
+      // f16x2: every layer leaves raw pre-activations; the next streamed
+      // layer scales and swishes them (act_swish) as it goes.
+      layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
+                NT == 2 ? 0 : (op.n_hidden > 1 || kLastSW) ? 1 : T);
+      // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
+      // biases seed the accumulators.  f16x2: they seed them divided by the
+      // unscale (exact: powers of two) and the accumulators are multiplied
+      // by it afterwards (kSeedScaled), or — ZF_X3_SEED_SCALED=0, hidden
+      // <= 128 — they join at the layer's end with the unscale in one fma
+      // (x3_finish; bias tiles live beside the accumulators there).
+      constexpr bool kSeedScaled = NT == 2 && (T == 8 || ZF_X3_SEED_SCALED);
+      for (int l = 1; l < op.n_hidden; ++l) {
+        floatx16 acc[T];
+        float isc = 1.f, us = 1.f, ius = 1.f;
+        if constexpr (NT == 2) {
+          x3_act_scale<T>(hb, op.x3_kw[l], isc, us, ius);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hb[0][r] = act_swish<NT>(hb[0][r], isc);
+        }
+#pragma unroll
+        for (int o = 0; o < T; ++o)
+          acc[o] = NT == 3 ? bias_acc(sp + op.b[l] + o * 32, hh)
+                           : (kSeedScaled ? bias_acc(sp + op.b[l] + o * 32, hh) * ius : floatx16{0});
+        const float* bh = (NT == 2 && !kSeedScaled) ? sp + op.b[l] : nullptr;
+        if constexpr (kPipe) {
+          typename XT<NT>::E cs[NT];
+          splitk<NT, 0>(hb[0], cs);
+          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us);
+        } else {
+          x3_layer<NT, T, T, true>(x3, pipe, hb, acc, lane, bh, hh, isc, us);
+        }
+        if constexpr (kSeedScaled) {
+#pragma unroll
+          for (int o = 0; o < T; ++o) acc[o] *= us;
+        }
+        const int nsw = NT == 2 ? 0 : (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
+#pragma unroll
+        for (int o = 0; o < T; ++o) {
+          if (o < nsw) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
+          } else {
+            hb[o] = acc[o];
+          }
+        }
+      }
+      // Last Dense (:346-347), one pair of transformed dims at a time: lane
+      // half h, tile o, register r = parameter 16*o + r of dim 2*pair + h.
+      const int dt = op.dt;
+      float ldn = 0.f;  // this coupling's log-det, summed in dim order (utils.py:139)
+      // PAIRS == false: one pair (dt <= 2), and the hidden activations are
+      // dead once the last layer has consumed them.
+      const int npair = PAIRS ? (dt + 1) / 2 : 1;
+      float lisc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
+      if constexpr (NT == 2) {
+        x3_act_scale<T>(hb, op.x3_kw[op.n_hidden], lisc, lus, lius);
+        // PAIRS: the input is read once per dim pair, so swish it whole here
+#pragma unroll
+        for (int o = 0; o < T; ++o)
+          if (o == 0 || !kLastSW)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hb[o][r] = act_swish<NT>(hb[o][r], lisc);
+      }
+      for (int pr = 0; pr < npair; ++pr) {
+        // The bias seeds the accumulators when the hidden activations stay
+        // live across pairs anyway; otherwise it joins in the last step, when
+        // the first input tiles are dead (fewer registers at the peak);
+        // f16x2 always joins it at the end, with the unscale.
+        const float* bl = sp + op.x3_blast + pr * TL * 32;
+        floatx16 pa[TL];
+        constexpr bool kSeed = PAIRS && NT == 3;
+#pragma unroll
+        for (int o = 0; o < TL; ++o)
+          pa[o] = kSeed ? bias_acc(bl + o * 32, hh) : (kSeedScaled ? bias_acc(bl + o * 32, hh) * lius : floatx16{0});
+        if constexpr (kPipe) {
+          typename XT<NT>::E cs[NT];
+          splitk<NT, 0>(hb[0], cs);
+          x3_layer_pipe<NT, T, TL, !kSeedScaled>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus);
+        } else {
+          x3_layer<NT, T, TL, kLastSW>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh, lisc, lus);
+        }
+        if constexpr (kSeedScaled) {
+#pragma unroll
+          for (int o = 0; o < TL; ++o) pa[o] *= lus;
+        }
+        float P[NPV];
+#pragma unroll
+        for (int o = 0; o < TL; ++o)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if constexpr (ONE) {  // both halves end up with all of the dim's parameters
+              const float other = __shfl_xor(pa[o][r], 32);
+              P[32 * o + r] = hh == 0 ? pa[o][r] : other;
+              P[32 * o + 16 + r] = hh == 0 ? other : pa[o][r];
+            } else {
+              P[16 * o + r] = pa[o][r];
+            }
+          }
+        // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
+        const int d = 2 * pr + hh;
+        const bool act = d < dt;  // the upper half idles on an odd last dim
+        float ldv = 0.f;
+        {
+          float w[K], hg[K];
+          float sx = 0.f, sy = 0.f;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
+            w[j] = x3_squareplus2(P[j]);
+            hg[j] = x3_squareplus2(P[K + j]);
+            sx = sx + w[j];
+            sy = sy + hg[j];
+          }
+          // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
+          // 2*squareplus: the same quotient bits): the parameters
+          // themselves already differ from the reference's in the last ulp
+          // (GEMM summation order), so correctly rounded divisions buy nothing.
+          const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
+          const float bc = kc.c * kc.rnorm;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            w[j] = __builtin_fmaf(w[j], ax, bc);
+            hg[j] = __builtin_fmaf(hg[j], ay, bc);
+          }
+          float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
+#pragma unroll
+          for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
+          float* xp = xs + wrap((act ? d : 0) + rot, D) * 32 + s;
+          const float xv = *xp;
+          const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
+                                                       [](float v) { return v == 0.f ? 1.f : x3_squareplus(v); });
+          float yv;
+          if (!INV) {
+            float l;
+            x3_forward_eval(xv, bin, yv, l);
+            ldv = act ? l : 0.f;
+          } else {
+            yv = rqs_inverse_eval(xv, bin);
+          }
+          if (act) *xp = yv;
+        }
+        wave_lds_sync();
+        if (!INV) {
+          const float other = __shfl_xor(ldv, 32);
+          ldn = ldn + (hh == 0 ? ldv : other);
+          if (2 * pr + 1 < dt) ldn = ldn + (hh == 0 ? other : ldv);
+        }
+      }
+      if (!INV) ld = ld + ldn;  // Chain: log_det += ld (bijectors.py:110)
+    }
+  }
+
+  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, nparts, y_out,
+                    ld_out, s_part);
+}
+
+template <int NT, int K, int T, bool PAIRS, bool ONE>
+int launch_x3(const X3Launch& a, bool inverse) {
+  const long long rows = kX3Waves * kTile;
+  const long long grid = (a.N + rows - 1) / rows;
+  if (grid > 0x7fffffffLL) return einval("N too large");
+  constexpr int TL = ONE ? (3 * K - 1 + 31) / 32 : (3 * K - 1 + 15) / 16;
+  const size_t lds = x3_lds_bytes(T > TL ? T : TL, a.D, NT);
+  if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
+  if (inverse)
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+                       a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
+                       a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
+  else
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+                       a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
+                       a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
+  ZF_CHECK_LAUNCH("flow_kernel_x3");
+  return ZF_OK;
+}
+
+// Instantiated shapes (x3_eligible): K in {8, 16, 32} at hidden 128 (T = 4)
+// and hidden 256 (T = 8).  PAIRS (a loop over transformed-dim pairs in the
+// last layer) whenever dt > 2, and always at T = 8 (its hidden activations
+// are live across the last layer anyway); ONE when dt == 1.
+template <int NT, int K>
+int launch_x3_k(const X3Launch& a, bool inverse) {
+  const int dt = a.D / 2;
+  const bool one = dt == 1;  // must match x3_pack's last-layer layout
+  if (a.T == 4) {
+    if (dt > 2) return launch_x3<NT, K, 4, true, false>(a, inverse);
+    return one ? launch_x3<NT, K, 4, false, true>(a, inverse) : launch_x3<NT, K, 4, false, false>(a, inverse);
+  }
+  if (a.T == 8)
+    return one ? launch_x3<NT, K, 8, true, true>(a, inverse) : launch_x3<NT, K, 8, true, false>(a, inverse);
+  return enotsup("split-MFMA kernel: hidden tiles not instantiated");
+}
+
+}  // namespace
+}  // namespace zf
