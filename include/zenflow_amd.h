@@ -287,12 +287,44 @@ int zf_trainer_loss_grad(zf_trainer_t* trainer, const float* x, const float* c, 
 int zf_trainer_step(zf_trainer_t* trainer, const float* x, const float* c, int64_t B, double* loss,
                     void* stream);
 
+/* Data-parallel training: one trainer per GPU, each
+ * on its shard of every global batch.  The trainer exchanges at every batch
+ * reduction of loss_fn and its gradient — the ShiftBounds batch min/max
+ * (bijectors.py:250-257), the BatchNorm batch sums forward and reverse
+ * (bijectors.py:342, flax BatchNorm), the loss (train.py:64-72) and the
+ * gradient (train.py:82) — through one primitive:
+ *   allgather(ctx, send, recv, bytes, stream): recv[world][bytes] = every
+ *   rank's `bytes` of send, in rank order, ordered on `stream`
+ * (zf_rccl_allgather with ctx = an RCCL communicator, or any host transport
+ * that completes it synchronously).  Every sum is a fixed tree over row
+ * leaves whose count depends on the global batch only, and the ranks combine
+ * their subtree roots by the top of that tree: every rank gets the same
+ * bits, and R ranks (a power of two, equal shards) the bits one device gets
+ * on the whole batch.  NULL / world 1: single device (the default). */
+typedef int (*zf_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes, void* stream);
+typedef struct zf_comm_desc {
+  int rank, world;
+  void* ctx;
+  zf_allgather_fn allgather;
+} zf_comm_desc;
+int zf_trainer_set_comm(zf_trainer_t* trainer, const zf_comm_desc* comm);
+
+/* loss_grad / step on this rank's `rows` rows of a global batch of
+ * `global_rows` rows (the loss is -mean over the global batch; the gradient
+ * and loss returned are the global ones, identical on every rank).  The
+ * plain entries above use global_rows = rows * world. */
+int zf_trainer_loss_grad_shard(zf_trainer_t* trainer, const float* x, const float* c, int64_t rows,
+                               int64_t global_rows, int update_stats, double* loss, float* grad, void* stream);
+int zf_trainer_step_shard(zf_trainer_t* trainer, const float* x, const float* c, int64_t rows, int64_t global_rows,
+                          double* loss, void* stream);
+
 /* Copy the trainer's natural blob (parameters + statistics) out / in. */
 int zf_trainer_get_blob(zf_trainer_t* trainer, float* blob_host);
 int zf_trainer_set_blob(zf_trainer_t* trainer, const float* blob_host);
 
 /* ------------------------------------------------------------------------ */
-/* RCCL (over xGMI) — all-reduce of the fp64 NLL partial across ranks.       */
+/* RCCL (over xGMI) — the NLL all-reduce of data-parallel log_prob and the  */
+/* trainer's all-gather.                                                      */
 /* ------------------------------------------------------------------------ */
 int zf_rccl_available(void);
 int zf_rccl_get_unique_id(char* id128);
@@ -300,6 +332,8 @@ int zf_rccl_comm_init(void** comm, int nranks, const char* id128, int rank);
 int zf_rccl_allreduce_sum_f64(void* comm, const double* send, double* recv, size_t count,
                               void* stream);
 int zf_rccl_comm_destroy(void* comm);
+/* zf_allgather_fn over RCCL (ncclAllGather of bytes): comm = ctx. */
+int zf_rccl_allgather(void* comm, const void* send, void* recv, size_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

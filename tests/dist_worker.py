@@ -1,4 +1,5 @@
-"""Rank program for the multi-process CPU tests (tests/test_dist_launch.py):
+"""Rank program for the multi-process tests (tests/test_dist_launch.py on
+CPU; tests/test_gpu_train_dp.py: ranks sharing the GPU):
 started by zenflow_amd.launch.spawn or by the tests' own torchrun-style
 launcher.  ``python tests/dist_worker.py <mode> <outdir>``; writes
 <outdir>/rank<r>.json."""
@@ -38,6 +39,12 @@ class OracleLogProbStep:
         return float(partial[0])
 
 
+def tree_data(rows):
+    """fp32 rows spanning 2^-40..2^40: fp64 sums of them depend on the order."""
+    rng = np.random.default_rng(3)
+    return (rng.standard_normal((rows, 5)) * np.exp2(rng.integers(-40, 40, (rows, 5)))).astype(np.float32)
+
+
 def main(mode, outdir):
     from tests.flowcases import make_case
     from zenflow_amd.dist import DataParallelLogProb, HostCommunicator, shard_rows
@@ -63,8 +70,53 @@ def main(mode, outdir):
         res["rows"] = b - a
         res["nll"] = dp.nll(n)
         res["lp"] = out.tolist()
+    elif mode == "tree":
+        # the trainer's reduction schedule on host data: this rank's subtree
+        # root, all-gathered, combined by the top of the tree
+        from zenflow_amd.dist import leaf_tree_colsum, tree_sum
+
+        Bg = int(os.environ.get("ZF_TEST_ROWS", "1024"))
+        x = tree_data(Bg)
+        a, b = shard_rows(Bg, rank, world)
+        root = leaf_tree_colsum(x[a:b], Bg, world)
+        parts = [np.frombuffer(p, np.float64) for p in rdzv.allgather_bytes(root.tobytes(), "roots")]
+        res["sum"] = tree_sum(parts).tobytes().hex()
+    elif mode == "train_dp":
+        _train_dp(rdzv, res, outdir)
     rdzv.close()
     Path(outdir, f"rank{rank}.json").write_text(json.dumps(res))
+
+
+def _train_dp(rdzv, res, outdir):
+    """One rank of data-parallel training on a shared GPU (HostAllgather):
+    loss_grad on this rank's shard, then ZF_TEST_STEPS optimiser steps;
+    the gradient, loss and final blob go to <outdir>/rank<r>.npz."""
+    from tests.flowcases import build_flow, make_case
+    from zenflow_amd.dist import HostAllgather, shard_rows
+    from zenflow_amd.train import Trainer
+
+    name, N, seed = os.environ["ZF_TEST_CASE"].split(":")
+    N, seed = int(N), int(seed)
+    steps = int(os.environ.get("ZF_TEST_STEPS", "3"))
+    case = make_case(name, N=N, seed=seed)
+    cfg = case["cfg"]
+    flow = build_flow(cfg)
+    flow.latent._dim = cfg["D"]
+    comm = HostAllgather(rdzv)
+    a, b = shard_rows(N, rdzv.rank, rdzv.world)
+    x = case["x"][a:b]
+    c = None if case["c"] is None else case["c"][a:b]
+    tr = Trainer(flow, case["variables"], cfg["D"], cfg["C"], b - a, comm=comm)
+    loss, g = tr.loss_grad(x, c, global_rows=N)
+    for _ in range(steps):
+        tr.step(x, c, global_rows=N)
+    blob = np.empty_like(tr.program.blob)
+    from zenflow_amd import _lib as L
+
+    L.check(L.load_library().zf_trainer_get_blob(tr.handle, blob.ctypes.data), "get_blob")
+    np.savez(Path(outdir, f"rank{rdzv.rank}.npz"), grad=g, loss=np.float64(loss), blob=blob,
+             last_loss=np.float64(tr.last_loss()))
+    res["rows"] = b - a
 
 
 if __name__ == "__main__":

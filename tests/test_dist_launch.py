@@ -93,3 +93,29 @@ def test_bench_rejects_mismatched_world():
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.parametrize("world,rows", [(2, 1024), (4, 1024), (2, 4096), (8, 2048)])
+def test_trainer_reduction_schedule_rank_invariant(tmp_path, world, rows):
+    """The trainer's batch-reduction schedule (leaves of ~32 rows whose count
+    depends on the global batch only, a pairwise fp64 tree, ranks combining
+    their subtree roots by the top of the tree; zenflow_amd.dist mirrors
+    zf_train.hip's leaves_for / tree_n): `world` ranks produce bit for bit the
+    one-device sum of the whole batch, on every rank."""
+    from zenflow_amd.dist import leaf_tree_colsum, reduction_leaves
+    from zenflow_amd.launch import spawn
+
+    n1, r1 = reduction_leaves(rows, rows, 1)
+    nw, rw = reduction_leaves(rows // world, rows, world)
+    assert n1 == nw * world and r1 == rw
+    env = dict(os.environ, ZF_TEST_ROWS=str(rows))
+    assert spawn(world, [WORKER, "tree", str(tmp_path)], env=env, timeout=120) == 0
+    res = _results(tmp_path, world)
+    from tests.dist_worker import tree_data
+
+    x = tree_data(rows)
+    one = leaf_tree_colsum(x, rows, 1).tobytes().hex()
+    assert all(r["sum"] == one for r in res)
+    # a different schedule (sequential fp64 sum) differs in the last bits here,
+    # so the equality above is not vacuous
+    assert np.asarray(x, np.float64).sum(axis=0).tobytes().hex() != one

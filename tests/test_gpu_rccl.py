@@ -48,3 +48,22 @@ def test_overlapped_allreduce_ring():
     # the ring's slots hold the last `depth` steps' all-reduced partials
     assert sorted(float(b.numpy()[0]) for b in ar.bufs) == sorted(vals[-4:].tolist())
     comm.close()
+
+
+def test_rccl_allgather_one_rank():
+    """zf_rccl_allgather (the trainer's zf_allgather_fn over RCCL) on a
+    one-rank communicator: recv = send."""
+    from zenflow_amd import _lib as L
+    from zenflow_amd._lib import DeviceArray
+    from zenflow_amd.dist import RcclCommunicator
+
+    comm = RcclCommunicator(0, 1, lambda b: b, force=True)
+    try:
+        src = DeviceArray.from_numpy(np.arange(37, dtype=np.float64))
+        dst = DeviceArray((37,), np.float64)
+        L.check(L.load_library().zf_rccl_allgather(comm.comm, src.ptr, dst.ptr, 37 * 8, L.stream()), "allgather")
+        assert np.array_equal(dst.numpy(), np.arange(37, dtype=np.float64))
+        d = comm.trainer_comm_desc()
+        assert d.world == 1 and d.allgather
+    finally:
+        comm.close()

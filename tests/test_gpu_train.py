@@ -107,6 +107,76 @@ def test_train_gradient_directional(name, N, seed):
             assert err <= 2e-3 * abs(an) + 2e-6, f"{name}/{label}: analytic {an} vs fd {fds}"
 
 
+def _leaves(tree, path=()):
+    if isinstance(tree, dict):
+        for k in sorted(tree):
+            yield from _leaves(tree[k], path + (k,))
+    else:
+        yield path, np.asarray(tree, np.float64)
+
+
+def _get(tree, path):
+    for k in path:
+        tree = tree[k]
+    return np.asarray(tree, np.float64)
+
+
+GRAD_CASES = CASES + [("cfg1", 1024, 66), ("d8", 512, 67), ("d2h256", 256, 68), ("odd", 300, 69)]
+
+
+@pytest.mark.parametrize("name,N,seed", GRAD_CASES)
+def test_train_gradient_per_parameter(name, N, seed):
+    """jax.grad of loss_fn (train.py:64-72, 82) per parameter: the GPU
+    trainer's fp32 reverse pass vs float64 autograd of the oracle's loss
+    (oracle/zf_oracle_torch.py).  Every element of every parameter tensor:
+    |g_gpu - g64| <= 1e-5 * max|g64| + 2 max(|g32 - g64|, |g64' - g64|)
+    (maxima over that tensor), where g32 is the same autograd in float32 over
+    three row orders of the batch (the rounding of the batch sums any fp32
+    evaluation, the reference's included, is subject to) and g64' the
+    float64 gradient at inputs and parameters jittered by ~4 fp32 ulp (its
+    conditioning: how far another fp32 per-row arithmetic can land)."""
+    import subprocess
+    import sys
+    import tempfile
+    from pathlib import Path
+
+    case, flow, tr = _setup(name, N, seed)
+    _, g = tr.loss_grad(case["x"], case["c"])
+    gg = tr.grad_tree(g)
+    # the autograd oracle runs in a CPU-only child (tests/grad_oracle.py)
+    root = Path(__file__).resolve().parents[1]
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "g.npz"
+        subprocess.run([sys.executable, "-m", "tests.grad_oracle", name, str(N), str(seed), str(out)], cwd=root,
+                       check=True, timeout=600)
+        ref = dict(np.load(out))
+    worst, bad = {}, []
+    for key in sorted(k for k in ref if k.startswith("g64:")):
+        path = tuple(key[4:].split("/"))
+        r64 = ref[key]
+        got = _get(gg, path)
+        assert got.shape == r64.shape, path
+        scale = max(np.abs(r64).max(), 1e-30)
+        e = np.abs(got - r64)
+        e32 = max(np.abs(ref[f"g32_{k}:" + key[4:]] - r64).max() for k in range(3))
+        cond = max(np.abs(ref[f"g64p_{k}:" + key[4:]] - r64).max() for k in range(2))
+        ok = e <= 1e-5 * scale + 2 * max(e32, cond)
+        worst["/".join(path)] = (float(e.max() / scale), float(e32 / scale), float(cond / scale))
+        if not ok.all():
+            bad.append(f"{'/'.join(path)}: {np.sum(~ok)} of {ok.size} over, max rel {e.max() / scale:.3g} "
+                       f"(fp32 autograd {e32 / scale:.3g}, conditioning {cond / scale:.3g})")
+    rel = max(v[0] for v in worst.values())
+    rel32 = max(v[1] for v in worst.values())
+    relc = max(v[2] for v in worst.values())
+    from tests.test_gpu_flow import _append_record
+
+    _append_record("grad_parity.jsonl", {"case": name, "rows": N, "leaves": len(worst),
+                                         "gpu_max_rel_err_vs_fp64": rel, "torch32_max_rel_err_vs_fp64": rel32,
+                                         "conditioning_max_rel": relc,
+                                         "over": bad})
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("nesterov", [True, False])
 def test_optimizer_step_matches_optax_formula(nesterov):
     from zenflow_amd.train import Optimizer

@@ -1,0 +1,45 @@
+"""Data-parallel training (train() with the cross-GPU
+reductions of ShiftBounds min/max, BatchNorm sums and the gradient;
+train.py:64-86, bijectors.py:250-257, :342).
+
+Two ranks share this box's one GPU (tests/dist_worker.py ``train_dp``; the
+trainer's all-gather goes through dist.HostAllgather, since RCCL refuses two
+ranks on one device), each on its half of every batch.  The trainer's batch
+reductions are fixed leaf trees whose shape depends on the global batch only,
+so both ranks must end with the bits ONE device gets on the whole batch:
+the same loss, the same gradient, and after three optimiser steps the same
+parameters and statistics — compared with ``array_equal``, not a tolerance."""
+
+import os
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_train import _setup
+
+pytestmark = pytest.mark.gpu
+WORKER = str(Path(__file__).resolve().parent / "dist_worker.py")
+
+
+@pytest.mark.parametrize("name,N,seed", [("cfg2", 1024, 81), ("cfg4", 2048, 82), ("d8", 1024, 83),
+                                         ("cfg2", 16384, 84)])
+def test_two_ranks_match_one_device_bitwise(tmp_path, name, N, seed):
+    from zenflow_amd import _lib as L
+    from zenflow_amd.launch import spawn
+
+    env = dict(os.environ, ZF_TEST_CASE=f"{name}:{N}:{seed}", ZF_TEST_STEPS="3")
+    assert spawn(2, [WORKER, "train_dp", str(tmp_path)], env=env, timeout=240) == 0
+    ranks = [np.load(tmp_path / f"rank{k}.npz") for k in range(2)]
+
+    case, flow, tr = _setup(name, N, seed)  # one device, the whole batch
+    loss, g = tr.loss_grad(case["x"], case["c"])
+    for _ in range(3):
+        tr.step(case["x"], case["c"])
+    blob = np.empty_like(tr.program.blob)
+    L.check(L.load_library().zf_trainer_get_blob(tr.handle, blob.ctypes.data), "get_blob")
+    for k, r in enumerate(ranks):
+        assert float(r["loss"]) == loss, f"rank {k} loss"
+        assert np.array_equal(r["grad"], g), f"rank {k}: {np.sum(r['grad'] != g)} gradient entries differ"
+        assert float(r["last_loss"]) == tr.last_loss(), f"rank {k} last loss"
+        assert np.array_equal(r["blob"], blob, equal_nan=True), f"rank {k}: {np.sum(r['blob'] != blob)} blob entries"

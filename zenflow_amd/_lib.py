@@ -58,6 +58,14 @@ class ZfOptimDesc(C.Structure):
                 ("weight_decay", C.c_float), ("nesterov", C.c_int)]
 
 
+# zf_allgather_fn(ctx, send, recv, bytes, stream) and zf_comm_desc
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class ZfCommDesc(C.Structure):
+    _fields_ = [("rank", C.c_int), ("world", C.c_int), ("ctx", C.c_void_p), ("allgather", C.c_void_p)]
+
+
 class ZfFlowDesc(C.Structure):
     _fields_ = [
         ("dim", C.c_int32),
@@ -120,6 +128,9 @@ SIGNATURES = {
     "zf_trainer_destroy": (_int, [_vp]),
     "zf_trainer_loss_grad": (_int, [_vp, _vp, _vp, _i64, _int, _vp, _vp, _vp]),
     "zf_trainer_step": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "zf_trainer_set_comm": (_int, [_vp, _vp]),
+    "zf_trainer_loss_grad_shard": (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp, _vp, _vp]),
+    "zf_trainer_step_shard": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _vp]),
     "zf_trainer_get_blob": (_int, [_vp, _vp]),
     "zf_trainer_set_blob": (_int, [_vp, _vp]),
     "zf_latent_sample": (_int, [_int, _dbl, _u64, _vp, _i64, _int, _vp]),
@@ -132,6 +143,7 @@ SIGNATURES = {
     "zf_rccl_comm_init": (_int, [C.POINTER(_vp), _int, C.c_char_p, _int]),
     "zf_rccl_allreduce_sum_f64": (_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
     "zf_rccl_comm_destroy": (_int, [_vp]),
+    "zf_rccl_allgather": (_int, [_vp, _vp, _vp, C.c_size_t, _vp]),
 }
 
 _lib: Optional[C.CDLL] = None

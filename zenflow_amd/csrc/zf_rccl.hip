@@ -1,6 +1,7 @@
-// RCCL (over xGMI) for the one real exchange step of data-parallel log_prob:
+// RCCL (over xGMI): the one real exchange step of data-parallel log_prob —
 // the all-reduce of the fp64 NLL partial sums (train.py:75-78 defines the NLL;
-// SURVEY.md §8e).  librccl is dlopen'ed lazily so loading libzenflow_amd.so
+// SURVEY.md §8e) — and the all-gather behind data-parallel training
+// (zf_trainer_set_comm).  librccl is dlopen'ed lazily so loading libzenflow_amd.so
 // never pulls RCCL into processes that do not need it.
 #include <dlfcn.h>
 
@@ -19,6 +20,7 @@ struct Rccl {
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   bool tried = false;
@@ -37,6 +39,7 @@ Rccl& rccl() {
       r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.lib, "ncclGetUniqueId");
       r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.lib, "ncclCommInitRank");
       r.all_reduce = (decltype(r.all_reduce))dlsym(r.lib, "ncclAllReduce");
+      r.all_gather = (decltype(r.all_gather))dlsym(r.lib, "ncclAllGather");
       r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.lib, "ncclCommDestroy");
       r.error_string = (decltype(r.error_string))dlsym(r.lib, "ncclGetErrorString");
     }
@@ -53,7 +56,7 @@ int nccl_status(ncclResult_t e, const char* what) {
 
 bool loaded() {
   Rccl& r = rccl();
-  return r.get_unique_id && r.comm_init_rank && r.all_reduce && r.comm_destroy;
+  return r.get_unique_id && r.comm_init_rank && r.all_reduce && r.all_gather && r.comm_destroy;
 }
 
 }  // namespace
@@ -91,6 +94,12 @@ int zf_rccl_allreduce_sum_f64(void* comm, const double* send, double* recv, size
   return zf::nccl_status(zf::rccl().all_reduce(send, recv, count, ncclFloat64, ncclSum,
                                                 (ncclComm_t)comm, (hipStream_t)stream),
                          "ncclAllReduce");
+}
+
+int zf_rccl_allgather(void* comm, const void* send, void* recv, size_t bytes, void* stream) {
+  if (!zf::loaded()) { zf::set_error("librccl not available"); return ZF_ENOTSUP; }
+  return zf::nccl_status(zf::rccl().all_gather(send, recv, bytes, ncclInt8, (ncclComm_t)comm, (hipStream_t)stream),
+                         "ncclAllGather");
 }
 
 int zf_rccl_comm_destroy(void* comm) {

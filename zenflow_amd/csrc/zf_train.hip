@@ -96,11 +96,18 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
       Bs[TB ? (e % MBK) : (e / BN)][TB ? (e / MBK) : (e % BN)] = rb[i];
     }
   };
-  floatx16 acc[TM][TN];
+  // NACC interleaved accumulator sets (k-pair s goes to set s % NACC),
+  // summed pairwise at the end: a 256-long fp32 fma chain becomes four
+  // 64-long ones (the input-gradient and forward GEMMs run K up to 256;
+  // the weight-gradient chunks are 32 rows).
+  constexpr int NACC = (WG || TM * TN > 1) ? 1 : 4;  // 128-wide tiles: registers for one set only
+  floatx16 acc[NACC][TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int q = 0; q < NACC; ++q)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = floatx16{0};
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[q][i][j] = floatx16{0};
   // bias-gradient column sums (WG, blockIdx.y == 0): column cc, k-quarter cq
   constexpr int CQ = 256 / BN, CK = MBK / CQ;
   const int cc = tid % BN, cq = tid / BN;
@@ -122,13 +129,23 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[(kb / 2) % NACC][i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[(kb / 2) % NACC][i][j], 0, 0, 0);
     }
     if (do_cs) {
 #pragma unroll
       for (int kk = 0; kk < CK; ++kk) csum += Bs[cq * CK + kk][cc];
     }
     __syncthreads();
+  }
+  if constexpr (NACC > 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[0][i][j] = NACC == 4 ? (acc[0][i][j] + acc[1][i][j]) + (acc[2][i][j] + acc[3][i][j])
+                                 : acc[0][i][j] + acc[1][i][j];
   }
   if (WG) {
     float* P = C + (long long)blockIdx.z * (M + 1) * N;
@@ -139,7 +156,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-          if (m < M && n < N) P[(long long)m * N + n] = acc[i][j][q];
+          if (m < M && n < N) P[(long long)m * N + n] = acc[0][i][j][q];
         }
     if (do_cs) {
       float* red = &As[0][0];  // free after the loop's last barrier
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
         const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
         if (m < M && n < N) {
           const long long o = (long long)m * ldc + n;
-          float v = acc[i][j][q];
+          float v = acc[0][i][j][q];
           if (epi == kEpiBias) {
             v = v + bias[n];
             if (H) H[o] = v * sigmoidf(v);
@@ -205,82 +222,136 @@ inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t 
 // Split-K workspace (floats) shared by the batch reductions below.
 constexpr int64_t kWsFloats = 8ll << 20;
 
-// Block: 32 consecutive elements x 8 split lanes; lane l sums splits
-// l, l+8, ... and the lanes combine in a fixed order.
-__global__ __launch_bounds__(256) void wgrad_final(int M, int N, int nsplit, const float* __restrict__ part,
-                                                   float* __restrict__ dW, float* __restrict__ db) {
-  __shared__ float red[8][33];
-  const int e = threadIdx.x & 31, l = threadIdx.x >> 5;
-  const long long idx = (long long)blockIdx.x * 32 + e;
+// ---- batch reductions: row leaves + one fixed pairwise tree ----------------
+// Every sum over the batch rows (weight and bias gradients, BatchNorm sums
+// forward and reverse, the loss) is formed the same way: the rows are cut
+// into n contiguous leaves of `rows` rows, each leaf is summed in row order,
+// and the leaves are combined in fp64 by the pairwise tree
+// ((l0 + l1) + (l2 + l3)) + ... (tree_n).  The global leaf count is a power of
+// two that depends on the GLOBAL batch size only (leaves_for); under data
+// parallelism rank r holds leaves [r n, (r+1) n) of it, reduces that subtree,
+// and the ranks' subtree roots are all-gathered and combined by the top of
+// the same tree.  So every rank gets the same bits, and R ranks reproduce
+// one rank's bits on the same global batch (R a power of two dividing the
+// leaf count, shards of B/R rows, B a multiple of the leaf count).
+constexpr int kMaxLeaves = 64;
+
+inline int pow2floor(long long v) {
+  int p = 1;
+  while ((long long)p * 2 <= v && p < (1 << 30)) p *= 2;
+  return p;
+}
+
+struct Leaves {
+  int n;     // this rank's leaves (a power of two)
+  int rows;  // rows per leaf (the last one may be short or empty)
+};
+
+// ~32 rows per leaf, at most `cap` (a power of two) leaves in the whole batch.
+inline Leaves leaves_for(long long B_loc, long long Bg, int world, int cap) {
+  const long long want = std::max<long long>(1, std::min<long long>(Bg / 32, cap));
+  Leaves l;
+  l.n = std::max(1, pow2floor(want / std::max(1, world)));
+  l.rows = (int)((B_loc + l.n - 1) / l.n);
+  return l;
+}
+
+// Pairwise tree over p[0], p[stride], ..., p[(n-1) stride] (n <= 64) in fp64:
+// level s adds element i + s into i for i a multiple of 2s (the perfect tree
+// for a power of two; a shorter tail just joins later).
+template <typename TI>
+__device__ __forceinline__ double tree_n(const TI* __restrict__ p, long long stride, int n) {
+  double v[kMaxLeaves];
+#pragma unroll
+  for (int i = 0; i < kMaxLeaves; ++i) v[i] = i < n ? (double)p[i * stride] : 0.0;
+#pragma unroll
+  for (int s = 1; s < kMaxLeaves; s *= 2)
+#pragma unroll
+    for (int i = 0; i < kMaxLeaves; i += 2 * s)
+      if (i + s < n) v[i] = v[i] + v[i + s];
+  return v[0];
+}
+
+// out[k] = tree over n leaves of part[leaf * N + k]
+template <typename TI>
+__global__ void tree_cols_kernel(const TI* __restrict__ part, int n, long long N, double* __restrict__ out) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < N) out[k] = tree_n(part + k, N, n);
+}
+
+// same, then the final fp32 rounding (the gradient handed to the optimiser)
+__global__ void tree_cols_cast_kernel(const double* __restrict__ part, int n, long long N, float* __restrict__ out) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < N) out[k] = (float)tree_n(part + k, N, n);
+}
+
+// dW/db from the split-K partials part[leaf][M+1][N] (fp32 leaf GEMMs),
+// combined by the leaf tree into the fp64 gradient accumulator.
+__global__ void wgrad_tree(int M, int N, int n, const float* __restrict__ part, double* __restrict__ dW,
+                           double* __restrict__ db) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long MN1 = (long long)(M + 1) * N;
-  float s = 0.f;
-  if (idx < MN1)
-    for (int k = l; k < nsplit; k += 8) s += part[k * MN1 + idx];
-  red[l][e] = s;
-  __syncthreads();
-  if (l == 0 && idx < MN1) {
-    const float v = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
-                    ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e]));
-    if (idx < (long long)M * N) dW[idx] = v;
-    else db[idx - (long long)M * N] = v;
-  }
+  if (idx >= MN1) return;
+  const double v = tree_n(part + idx, MN1, n);
+  if (idx < (long long)M * N) dW[idx] = v;
+  else db[idx - (long long)M * N] = v;
 }
 
 // dW[M,N] = A^T . G and db[N] = colsum(G), A row-major [B][M] (layer input),
-// G row-major [B][N] (gradient of the layer output); the split partials are
-// summed in a fixed order by wgrad_final, so the result is deterministic.
-int wgrad(int M, int N, int B, const float* A, const float* G, float* dW, float* db, float* ws, hipStream_t st) {
+// G row-major [B][N] (gradient of the layer output): one split-K block per
+// leaf (rows [z lv.rows, (z+1) lv.rows)), then wgrad_tree.
+int wgrad(int M, int N, int B, const Leaves& lv, const float* A, const float* G, double* dW, double* db, float* ws,
+          hipStream_t st) {
   constexpr int T = 64;
-  // ~2048 blocks in flight, partials within the workspace
-  const int tiles = ((N + T - 1) / T) * ((M + T - 1) / T);
-  int nsplit = (int)std::min<int64_t>(std::min<int64_t>((B + MBK - 1) / MBK, std::max(1, 2048 / tiles)),
-                                      kWsFloats / ((int64_t)(M + 1) * N));
-  nsplit = nsplit < 1 ? 1 : nsplit;
-  int KC = (B + nsplit - 1) / nsplit;
-  KC = (KC + MBK - 1) / MBK * MBK;
-  nsplit = (B + KC - 1) / KC;
-  hipLaunchKernelGGL((mgemm_kernel<T, T, true, false, true>), dim3((N + T - 1) / T, (M + T - 1) / T, nsplit),
-                     dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, KC);
+  if ((int64_t)lv.n * (M + 1) * N > kWsFloats) return enotsup("training: weight-gradient workspace");
+  hipLaunchKernelGGL((mgemm_kernel<T, T, true, false, true>), dim3((N + T - 1) / T, (M + T - 1) / T, lv.n),
+                     dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows);
   ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
-  hipLaunchKernelGGL(wgrad_final, dim3(blocks_for((int64_t)(M + 1) * N, 32)), dim3(256), 0, st, M, N, nsplit, ws, dW, db);
-  ZF_CHECK_LAUNCH("wgrad_final");
+  hipLaunchKernelGGL(wgrad_tree, dim3(blocks_for((int64_t)(M + 1) * N)), dim3(256), 0, st, M, N, lv.n, ws, dW, db);
+  ZF_CHECK_LAUNCH("wgrad_tree");
   return ZF_OK;
 }
 
-// ---- per-column sums (split over row chunks, fixed-order final sum) ---------
-// out[n] = sum_b X[b, n] * (Y ? Y[b, n] : 1), N <= 64 columns.
-constexpr int kColChunk = 256;
-
-__global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ X, const float* __restrict__ Y, int B,
-                                                      int N, float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int n = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int b0 = blockIdx.x * kColChunk, b1 = min(B, b0 + kColChunk);
-  float s = 0.f;
-  if (n < N)
-    for (int b = b0 + rg; b < b1; b += 4) {
-      const float x = X[(long long)b * N + n];
-      s += Y ? x * Y[(long long)b * N + n] : x;
-    }
-  red[rg][n] = s;
-  __syncthreads();
-  if (rg == 0 && n < N) part[(long long)blockIdx.x * N + n] = (red[0][n] + red[1][n]) + (red[2][n] + red[3][n]);
+// Leaf sums of two per-column sums over rows [b0, b1), in row order, fp64:
+// s1 = sum x, s2 = sum x * y (y = x: the sum of squares).
+template <class FX, class FY>
+__device__ __forceinline__ void leaf_sums2(FX x_at, FY y_at, int b0, int b1, double& s1, double& s2) {
+  double a = 0.0, q = 0.0;
+  for (int b = b0; b < b1; ++b) {
+    const double xv = (double)x_at(b), yv = (double)y_at(b);
+    a += xv;
+    q += xv * yv;
+  }
+  s1 = a;
+  s2 = q;
 }
 
-__global__ void colsum_final(const float* __restrict__ part, int nblk, int N, float* __restrict__ out) {
-  const int n = threadIdx.x;
-  if (n >= N) return;
-  double s = 0.0;
-  for (int k = 0; k < nblk; ++k) s += (double)part[(long long)k * N + n];
-  out[n] = (float)s;
+// One thread per (leaf z, column k): p[z][k] = sum x, p[z][N + k] = sum x*y
+// over the leaf's rows of X, Y row-major [B][N] (Y NULL: Y = X).
+__global__ void leaf_colsums_kernel(const float* __restrict__ X, const float* __restrict__ Y, int B, int N, int rows,
+                                    int n, double* __restrict__ p) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * N) return;
+  const int z = t / N, k = t - z * N;
+  const int b0 = min(B, z * rows), b1 = min(B, b0 + rows);
+  const float* Yp = Y ? Y : X;
+  leaf_sums2([&](int b) { return X[(long long)b * N + k]; }, [&](int b) { return Yp[(long long)b * N + k]; }, b0, b1,
+             p[(long long)z * 2 * N + k], p[(long long)z * 2 * N + N + k]);
 }
 
-int colsum(const float* X, const float* Y, int B, int N, float* out, float* ws, hipStream_t st) {
-  const int nblk = (B + kColChunk - 1) / kColChunk;
-  hipLaunchKernelGGL(colsum_partial, dim3(nblk), dim3(256), 0, st, X, Y, B, N, ws);
-  ZF_CHECK_LAUNCH("colsum_partial");
-  hipLaunchKernelGGL(colsum_final, dim3(1), dim3(64), 0, st, ws, nblk, N, out);
-  ZF_CHECK_LAUNCH("colsum_final");
+// Leaf sums of one column vector (the per-row loss), fp64 in row order.
+__global__ void leaf_sum_kernel(const double* __restrict__ x, int B, int rows, int n, double* __restrict__ p) {
+  const int z = blockIdx.x * blockDim.x + threadIdx.x;
+  if (z >= n) return;
+  const int b0 = min(B, z * rows), b1 = min(B, b0 + rows);
+  double a = 0.0;
+  for (int b = b0; b < b1; ++b) a += x[b];
+  p[z] = a;
+}
+
+inline int launch_tree_cols(const double* part, int n, long long N, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(tree_cols_kernel<double>, dim3(blocks_for(N)), dim3(256), 0, st, part, n, N, out);
+  ZF_CHECK_LAUNCH("tree_cols_kernel");
   return ZF_OK;
 }
 
@@ -353,20 +424,57 @@ __global__ void gather_u_kernel(const float* __restrict__ s, const float* __rest
 // BatchNorm with batch statistics (flax, use_running_average=False):
 // mean, var = max(0, E[u^2] - E[u]^2); u_hat = (u - mean) * rsqrt(var + eps);
 // u_bn = u_hat * scale + bias.  Also the running-average update (momentum 0.99).
-__global__ void bn_stats_kernel(const double* __restrict__ csum, const double* __restrict__ csq, int B, int DC,
-                                float* __restrict__ nat_bn, float* __restrict__ mean_out,
-                                float* __restrict__ rstd_out, int update) {
-  const int k = threadIdx.x;
-  if (k >= DC) return;
-  const float mean = (float)(csum[k] / B);
-  const float mean2 = (float)(csq[k] / B);
+// sum / sumsq: fp64 column sums over the global batch of Bg rows.
+__device__ __forceinline__ void bn_stats_one(double sum, double sumsq, long long Bg, int k, int DC,
+                                             float* __restrict__ nat_bn, float& mean, float& rstd, int update) {
+#pragma clang fp contract(off)
+  // every operation separately rounded: the same bits in every kernel that inlines this
+  mean = (float)(sum / Bg);
+  const float mean2 = (float)(sumsq / Bg);
   const float var = fmaxf(0.f, mean2 - mean * mean);
-  mean_out[k] = mean;
-  rstd_out[k] = 1.0f / sqrtf(var + kBnEps);
+  rstd = 1.0f / sqrtf(var + kBnEps);
   if (update) {
     nat_bn[k] = kBnMomentum * nat_bn[k] + (1.0f - kBnMomentum) * mean;
     nat_bn[DC + k] = kBnMomentum * nat_bn[DC + k] + (1.0f - kBnMomentum) * var;
   }
+}
+
+__global__ void bn_stats_kernel(const double* __restrict__ csum, const double* __restrict__ csq, long long Bg, int DC,
+                                float* __restrict__ nat_bn, float* __restrict__ mean_out,
+                                float* __restrict__ rstd_out, int update) {
+  const int k = threadIdx.x;
+  if (k >= DC) return;
+  float mean, rstd;
+  bn_stats_one(csum[k], csq[k], Bg, k, DC, nat_bn, mean, rstd, update);
+  mean_out[k] = mean;
+  rstd_out[k] = rstd;
+}
+
+// Per-element BatchNorm arithmetic shared by the single-block and the
+// multi-launch paths, every operation separately rounded (fp contraction off:
+// HIP's __f*_rn are plain operators that the compiler may still fuse, and it
+// fuses differently in different kernels): both paths give the same bits.
+__device__ __forceinline__ float bn_hat(float u, float mean, float rstd) {
+#pragma clang fp contract(off)
+  return (u - mean) * rstd;
+}
+__device__ __forceinline__ float bn_out(float uh, float scale, float bias) {
+#pragma clang fp contract(off)
+  return uh * scale + bias;
+}
+// reverse: the mean terms scale * sum / Bg, then
+// dL/dU = rstd * (gUbn * scale - mg - Uhat * mgu)
+__device__ __forceinline__ float bn_mean_term(float scale, double sum, long long Bg) {
+#pragma clang fp contract(off)
+  return scale * (float)sum / (float)Bg;
+}
+__device__ __forceinline__ float bn_grad_in(float gubn, float uh, float scale, float rstd, float mg, float mgu) {
+#pragma clang fp contract(off)
+  return rstd * (gubn * scale - mg - uh * mgu);
+}
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
 }
 
 __global__ void bn_apply_kernel(const float* __restrict__ U, const float* __restrict__ mean,
@@ -376,9 +484,9 @@ __global__ void bn_apply_kernel(const float* __restrict__ U, const float* __rest
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)B * DC) return;
   const int k = (int)(i % DC);
-  const float uh = (U[i] - mean[k]) * rstd[k];
+  const float uh = bn_hat(U[i], mean[k], rstd[k]);
   Uhat[i] = uh;
-  Ubn[i] = uh * scale[k] + bias[k];
+  Ubn[i] = bn_out(uh, scale[k], bias[k]);
 }
 
 __device__ __forceinline__ float sp_f(float x) { return 0.5f * (x + sqrtf(x * x + 4.0f)); }
@@ -599,60 +707,46 @@ __global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __
 // gU = rstd * (gUhat - mean(gUhat) - u_hat * mean(gUhat * u_hat)), gUhat = gUbn * scale.
 __global__ void bn_bwd_kernel(const float* __restrict__ gUbn, const float* __restrict__ Uhat,
                               const float* __restrict__ scale, const float* __restrict__ rstd,
-                              const float* __restrict__ sum_g, const float* __restrict__ sum_gu,
-                              float* __restrict__ gU, int B, int DC) {
+                              const double* __restrict__ sum_g, const double* __restrict__ sum_gu,
+                              float* __restrict__ gU, int B, long long Bg, int DC) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)B * DC) return;
   const int k = (int)(i % DC);
-  // sum_g / sum_gu are sums of gUbn and gUbn*Uhat; scale them into gUhat terms
-  const float mg = scale[k] * sum_g[k] / B, mgu = scale[k] * sum_gu[k] / B;
-  gU[i] = rstd[k] * (gUbn[i] * scale[k] - mg - Uhat[i] * mgu);
+  // sum_g / sum_gu: global sums of gUbn and gUbn*Uhat; scaled into gUhat terms
+  const float mg = bn_mean_term(scale[k], sum_g[k], Bg), mgu = bn_mean_term(scale[k], sum_gu[k], Bg);
+  gU[i] = bn_grad_in(gUbn[i], Uhat[i], scale[k], rstd[k], mg, mgu);
 }
 
 // ---- small batches: BatchNorm forward / reverse in one single-block launch --
-// (B * DC <= kBnSmall).  Same arithmetic as gather_u + colstats + bn_stats +
-// bn_apply (forward) and colsum x2 + bn_bwd + scatter (reverse); the column
-// sums are fp64 over a fixed thread layout (column k = tid % DC, row lane
-// tid / DC) combined in lane order, so the result is deterministic.
+// (B * DC <= kBnSmall, one device).  The same arithmetic as the multi-launch
+// path (gather_u + leaf_colsums + tree + bn_stats + bn_apply forward;
+// leaf_colsums + tree + bn_bwd + scatter reverse): the same leaf_sums2 per
+// (leaf, column) and the same tree_n over the leaves, here through LDS.
 constexpr long long kBnSmall = 1ll << 14;
+constexpr int kBnLeafCap = kMaxLeaves;  // leaves of a BatchNorm sum (both paths)
 
 __global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s, const float* __restrict__ c,
                                                      float* __restrict__ Uhat, float* __restrict__ Ubn,
                                                      float* __restrict__ nat_bn, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int B, int D, int C, int dt, int dc,
-                                                     int rot, int update) {
-  __shared__ double ssum[1024], ssq[1024];
+                                                     int rot, int n, int rows, int update) {
+  __shared__ double p1[kMaxLeaves * 64], p2[kMaxLeaves * 64];
   __shared__ float smean[64], srstd[64];
-  const int DC = dc + C, L = 1024 / DC, tid = threadIdx.x;
-  const int k = tid % DC, l = tid / DC;
+  const int DC = dc + C, tid = threadIdx.x;
   auto u_at = [&](long long b, int kk) { return kk < dc ? s[b * D + pmodi(dt + kk + rot, D)] : c[b * C + (kk - dc)]; };
-  double sm = 0.0, sq = 0.0;
-  if (l < L)
-    for (long long b = l; b < B; b += L) {
-      const double u = (double)u_at(b, k);
-      sm += u;
-      sq += u * u;
-    }
-  ssum[tid] = sm;
-  ssq[tid] = sq;
+  for (int t = tid; t < n * DC; t += 1024) {
+    const int z = t / DC, k = t - z * DC;
+    const int b0 = min(B, z * rows), b1 = min(B, b0 + rows);
+    leaf_sums2([&](int b) { return u_at(b, k); }, [&](int b) { return u_at(b, k); }, b0, b1, p1[t], p2[t]);
+  }
   __syncthreads();
   if (tid < DC) {
-    double a = 0.0, q = 0.0;
-    for (int j = 0; j < L; ++j) {
-      a += ssum[j * DC + tid];
-      q += ssq[j * DC + tid];
-    }
-    const float mean = (float)(a / B), mean2 = (float)(q / B);
-    const float var = fmaxf(0.f, mean2 - mean * mean);
-    const float rstd = 1.0f / sqrtf(var + kBnEps);
+    float mean, rstd;
+    bn_stats_one(tree_n(p1 + tid, DC, n), tree_n(p2 + tid, DC, n), B, tid, DC, nat_bn, mean, rstd, update);
     smean[tid] = mean;
     srstd[tid] = rstd;
     mean_out[tid] = mean;
     rstd_out[tid] = rstd;
-    if (update) {
-      nat_bn[tid] = kBnMomentum * nat_bn[tid] + (1.0f - kBnMomentum) * mean;
-      nat_bn[DC + tid] = kBnMomentum * nat_bn[DC + tid] + (1.0f - kBnMomentum) * var;
-    }
   }
   __syncthreads();
   const float* scale = nat_bn + 2 * DC;
@@ -660,52 +754,46 @@ __global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s
   for (long long i = tid; i < (long long)B * DC; i += 1024) {
     const long long b = i / DC;
     const int kk = (int)(i - b * DC);
-    const float uh = (u_at(b, kk) - smean[kk]) * srstd[kk];
+    const float uh = bn_hat(u_at(b, kk), smean[kk], srstd[kk]);
     Uhat[i] = uh;
-    Ubn[i] = uh * scale[kk] + bias[kk];
+    Ubn[i] = bn_out(uh, scale[kk], bias[kk]);
   }
 }
 
-// gUbn = dL/dUbn -> BatchNorm scale / bias gradients and dL/dU; the
-// conditioning columns' share is added to g (dL/d state) in place.
+// gUbn = dL/dUbn -> BatchNorm scale / bias gradients (fp64 accumulator) and
+// dL/dU; the conditioning columns' share is added to g (dL/d state) in place.
 __global__ __launch_bounds__(1024) void bn_bwd_small(const float* __restrict__ gUbn, const float* __restrict__ Uhat,
                                                      const float* __restrict__ scale, const float* __restrict__ rstd,
-                                                     float* __restrict__ g_scale, float* __restrict__ g_bias,
+                                                     double* __restrict__ g_scale, double* __restrict__ g_bias,
                                                      float* __restrict__ g, int B, int D, int C, int dt, int dc,
-                                                     int rot) {
-  __shared__ double sgu[1024], sg[1024];
+                                                     int rot, int n, int rows) {
+  __shared__ double p1[kMaxLeaves * 64], p2[kMaxLeaves * 64];
   __shared__ float mg_s[64], mgu_s[64];
-  const int DC = dc + C, L = 1024 / DC, tid = threadIdx.x;
-  const int k = tid % DC, l = tid / DC;
-  double a = 0.0, q = 0.0;
-  if (l < L)
-    for (long long b = l; b < B; b += L) {
-      const float gv = gUbn[b * DC + k];
-      a += (double)(gv * Uhat[b * DC + k]);
-      q += (double)gv;
-    }
-  sgu[tid] = a;
-  sg[tid] = q;
+  const int DC = dc + C, tid = threadIdx.x;
+  for (int t = tid; t < n * DC; t += 1024) {
+    const int z = t / DC, k = t - z * DC;
+    const int b0 = min(B, z * rows), b1 = min(B, b0 + rows);
+    leaf_sums2([&](int b) { return gUbn[(long long)b * DC + k]; }, [&](int b) { return Uhat[(long long)b * DC + k]; },
+               b0, b1, p1[t], p2[t]);
+  }
   __syncthreads();
   if (tid < DC) {
-    double x = 0.0, y = 0.0;
-    for (int j = 0; j < L; ++j) {
-      x += sgu[j * DC + tid];
-      y += sg[j * DC + tid];
-    }
-    const float sum_gu = (float)x, sum_g = (float)y;
-    g_scale[tid] = sum_gu;
-    g_bias[tid] = sum_g;
-    mg_s[tid] = scale[tid] * sum_g / B;
-    mgu_s[tid] = scale[tid] * sum_gu / B;
+    const double sg = tree_n(p1 + tid, DC, n), sgu = tree_n(p2 + tid, DC, n);
+    g_scale[tid] = sgu;
+    g_bias[tid] = sg;
+    mg_s[tid] = bn_mean_term(scale[tid], sg, B);
+    mgu_s[tid] = bn_mean_term(scale[tid], sgu, B);
   }
   __syncthreads();
   for (long long i = tid; i < (long long)B * dc; i += 1024) {
     const long long b = i / dc;
     const int kk = (int)(i - b * dc);
     const long long e = b * DC + kk;
-    const float gu = rstd[kk] * (gUbn[e] * scale[kk] - mg_s[kk] - Uhat[e] * mgu_s[kk]);
-    g[b * D + pmodi(dt + kk + rot, D)] += gu;
+    const float gu = bn_grad_in(gUbn[e], Uhat[e], scale[kk], rstd[kk], mg_s[kk], mgu_s[kk]);
+    // a separately rounded add (no fma with the product above), as the
+    // multi-launch path's scatter_gu_kernel adds a stored gU
+    float* gp = g + b * D + pmodi(dt + kk + rot, D);
+    *gp = add_rn(*gp, gu);
   }
 }
 
@@ -716,18 +804,18 @@ __global__ void scatter_gu_kernel(const float* __restrict__ gU, float* __restric
   if (i >= (long long)B * dc) return;
   const long long b = i / dc;
   const int k = (int)(i - b * dc);
-  g[b * D + pmodi(dt + k + rot, D)] += gU[b * DC + k];
+  float* gp = g + b * D + pmodi(dt + k + rot, D);
+  *gp = add_rn(*gp, gU[b * DC + k]);
 }
 
 // ---- latent + loss ------------------------------------------------------------
-// lp = latent.log_prob(z) + log_det, nan_to_num (flow.py:45-47); loss partials
-// -lp/B (fp64); gz = -(1/B) d latent_lp / dz (zero where lp is not finite).
-__global__ void latent_loss_kernel(const float* __restrict__ z, const float* __restrict__ ld, int B, int D, int rot,
-                                   int latent, float a, float betac, float tnmass, float* __restrict__ gz,
-                                   double* __restrict__ partial) {
-  __shared__ double sm[256];
+// lp = latent.log_prob(z) + log_det, nan_to_num (flow.py:45-47); per-row
+// loss terms -lp/Bg (fp64, summed by the leaf tree); gz = -(1/Bg) d latent_lp
+// / dz (zero where lp is not finite).  Bg: the global batch size.
+__global__ void latent_loss_kernel(const float* __restrict__ z, const float* __restrict__ ld, int B, long long Bg,
+                                   int D, int rot, int latent, float a, float betac, float tnmass,
+                                   float* __restrict__ gz, double* __restrict__ row_loss) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  double contrib = 0.0;
   if (b < B) {
     float lat = 0.f;
     for (int j = 0; j < D; ++j) {
@@ -754,8 +842,8 @@ __global__ void latent_loss_kernel(const float* __restrict__ z, const float* __r
     if (lp != lp) lp = -INFINITY;
     if (lp == INFINITY) lp = 3.40282347e38f;
     if (lp == -INFINITY) lp = -3.40282347e38f;
-    contrib = -(double)lp / B;
-    const float s = -1.0f / B;
+    row_loss[b] = -(double)lp / (double)Bg;
+    const float s = -1.0f / (float)Bg;
     for (int j = 0; j < D; ++j) {
       const int col = pmodi(j + rot, D);
       const float v = z[(long long)b * D + col];
@@ -767,20 +855,27 @@ __global__ void latent_loss_kernel(const float* __restrict__ z, const float* __r
       gz[(long long)b * D + col] = s * g;
     }
   }
-  sm[threadIdx.x] = contrib;
-  __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if ((int)threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial[blockIdx.x] = sm[0];
 }
 
-__global__ void sum_partials_kernel(const double* __restrict__ part, int n, double* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < n; ++i) s += part[i];
-  out[0] = s;
+// ShiftBounds batch min / max of every rank (all-gathered [world][2][64]:
+// min row, max row) -> the global min / max (a NaN anywhere stays NaN).
+__global__ void minmax_ranks_kernel(const float* __restrict__ gath, int world, int D, float* __restrict__ cmin,
+                                    float* __restrict__ cmax) {
+  const int i = threadIdx.x;
+  if (i >= D) return;
+  float lo = gath[i], hi = gath[64 + i];
+  for (int r = 1; r < world; ++r) {
+    const float a = gath[r * 128 + i], b = gath[r * 128 + 64 + i];
+    lo = (lo != lo || a != a) ? __builtin_nanf("") : fminf(lo, a);
+    hi = (hi != hi || b != b) ? __builtin_nanf("") : fmaxf(hi, b);
+  }
+  cmin[i] = lo;
+  cmax[i] = hi;
+}
+
+__global__ void cast_f64_f32_kernel(const double* __restrict__ x, long long n, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (float)x[i];
 }
 
 // ---- optimiser: optax adamw / nadamw ---------------------------------------
@@ -844,12 +939,19 @@ struct zf_trainer {
   hipStream_t cap = nullptr;
   std::map<int64_t, hipGraphExec_t> graphs;
   bool use_graph = true;
+  bool bn_small = true;  // ZF_TRAIN_BN_SMALL=0: always the multi-launch BatchNorm path
   float* d_ld = nullptr;      // [bmax]
   float* d_g0 = nullptr;      // [bmax][D]
   float* d_g1 = nullptr;
-  float* d_small = nullptr;   // per-column scratch
-  double* d_dsmall = nullptr;
-  double* d_part = nullptr;
+  float* d_small = nullptr;   // per-column scratch (ShiftBounds min / max)
+  double* d_leaf = nullptr;   // leaf partials of the BatchNorm sums / loss [kMaxLeaves][128]
+  double* d_roots = nullptr;  // [0,128): tree roots of one reduction; [128]: the loss
+  double* d_rowloss = nullptr;  // [bmax] per-row loss terms
+  double* d_g64 = nullptr;    // fp64 gradient accumulator (blob layout)
+  // data parallelism: the communicator and its all-gather landing buffer
+  zf_comm_desc comm{0, 1, nullptr, nullptr};
+  void* d_gath = nullptr;
+  int64_t gath_bytes = 0;
   void* d_colws = nullptr;
   float* d_ws = nullptr;      // split-K partials (kWsFloats)
   int64_t colws_bytes = 0;
@@ -936,14 +1038,18 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_g0 = zf::dmalloc(t, B * D, rc);
   t->d_g1 = zf::dmalloc(t, B * D, rc);
   t->d_small = zf::dmalloc(t, 8 * 256, rc);
-  t->d_dsmall = (double*)zf::dmalloc(t, 4 * 256, rc);
-  t->d_part = (double*)zf::dmalloc(t, 2 * ((B + 255) / 256 + 1), rc);
+  t->d_leaf = (double*)zf::dmalloc(t, 2 * zf::kMaxLeaves * 128, rc);
+  t->d_roots = (double*)zf::dmalloc(t, 2 * 256, rc);
+  t->d_rowloss = (double*)zf::dmalloc(t, 2 * B, rc);
+  t->d_g64 = (double*)zf::dmalloc(t, 2 * need, rc);
   t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
   t->d_c = zf::dmalloc(t, B * (desc.cond_dim > 0 ? desc.cond_dim : 1), rc);
   t->d_bc = zf::dmalloc(t, 4, rc);
   {
     const char* g = std::getenv("ZF_TRAIN_GRAPH");
     t->use_graph = !(g && g[0] == '0');
+    const char* bs = std::getenv("ZF_TRAIN_BN_SMALL");
+    t->bn_small = !(bs && bs[0] == '0');
   }
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&t->cap, hipStreamNonBlocking);
@@ -996,7 +1102,29 @@ int zf_trainer_destroy(zf_trainer_t* t) {
   for (auto& kv : t->graphs) (void)hipGraphExecDestroy(kv.second);
   if (t->cap) (void)hipStreamDestroy(t->cap);
   for (float* p : t->bufs) (void)hipFree(p);
+  if (t->d_gath) (void)hipFree(t->d_gath);
   delete t;
+  return ZF_OK;
+}
+
+int zf_trainer_set_comm(zf_trainer_t* t, const zf_comm_desc* comm) {
+  if (!t) return zf::einval("trainer is NULL");
+  zf_comm_desc c{0, 1, nullptr, nullptr};
+  if (comm) c = *comm;
+  if (c.world < 1 || c.rank < 0 || c.rank >= c.world) return zf::einval("bad rank %d / world %d", c.rank, c.world);
+  if (c.world > zf::kMaxLeaves) return zf::enotsup("training: more than 64 ranks");
+  if (c.world > 1 && !c.allgather) return zf::einval("communicator without allgather");
+  ZF_TRY_HIP(hipDeviceSynchronize());
+  if (t->d_gath) (void)hipFree(t->d_gath);
+  t->d_gath = nullptr;
+  t->gath_bytes = 0;
+  if (c.world > 1) {
+    // largest exchange: the fp64 gradient of every rank
+    const int64_t per = std::max<int64_t>(t->nat_floats, 256) * (int64_t)sizeof(double);
+    t->gath_bytes = per * c.world;
+    ZF_TRY_HIP(hipMalloc(&t->d_gath, (size_t)t->gath_bytes));
+  }
+  t->comm = c;
   return ZF_OK;
 }
 
@@ -1017,15 +1145,29 @@ int trainer_stage(zf_trainer_t* t, const float* x, const float* c, int64_t B64, 
   return ZF_OK;
 }
 
-inline double* loss_slot(zf_trainer_t* t, int B) { return t->d_part + blocks_for(B); }
+inline double* loss_slot(zf_trainer_t* t) { return t->d_roots + 128; }
 
-// Train-mode forward + loss + reverse pass from the staged batch; the loss
-// lands in loss_slot(t, B), the gradient in G (natural blob layout).
-int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t st) {
-  const int D = t->D, C = t->C;
+// Data parallelism: this rank's tree roots (n doubles, in place) -> the
+// global ones: all-gather every rank's roots, combine them by the top of the
+// leaf tree (tree_n over ranks).  Nothing to do on one device.
+int dp_combine(zf_trainer_t* t, double* roots, long long n, hipStream_t st) {
+  const int W = t->comm.world;
+  if (W <= 1) return ZF_OK;
+  if ((int64_t)n * (int64_t)sizeof(double) * W > t->gath_bytes) return einval("all-gather buffer too small");
+  const int rc = t->comm.allgather(t->comm.ctx, roots, t->d_gath, (size_t)n * sizeof(double), st);
+  if (rc) return rc;
+  return launch_tree_cols((const double*)t->d_gath, W, n, roots, st);
+}
+
+// Train-mode forward + loss + reverse pass from the staged batch of B rows
+// (this rank's shard of a global batch of Bg rows); the loss lands in
+// loss_slot(t), the gradient in G (natural blob layout, fp32).
+int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* G, hipStream_t st) {
+  const int D = t->D, C = t->C, W = t->comm.world;
   const float* c = t->d_c;
   const zf_flow_desc& desc = t->desc;
   float* nat = t->d_nat;
+  double* G64 = t->d_g64;
   // state before op i; Roll is an index rotation, so it aliases its input
   std::vector<float*> sp(desc.n_ops + 1);
   sp[0] = t->d_state;
@@ -1033,6 +1175,9 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
     sp[i + 1] = desc.ops[i].kind == ZF_OP_ROLL ? sp[i] : t->d_state + (int64_t)(i + 1) * t->bmax * D;
   auto state = [&](int i) { return sp[i]; };
   ZF_TRY_HIP(hipMemsetAsync(t->d_ld, 0, (size_t)B * sizeof(float), st));
+  const Leaves lbn = leaves_for(B, Bg, W, kBnLeafCap);
+  // the single-block BatchNorm kernels have no exchange point (one device only)
+  const bool small_ok = W == 1 && t->bn_small;
   int rc;
   // ---- forward (train mode) ----
   int rot = 0;
@@ -1050,6 +1195,13 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
       rc = zf_colstats(sin, B, D, D, 0, t->sb_modes.data(), t->sb_prm.data(), t->d_small, t->d_small + 64,
                        nullptr, nullptr, t->d_colws, st);
       if (rc) return rc;
+      if (W > 1) {  // min / max over all ranks (exact in any order)
+        rc = t->comm.allgather(t->comm.ctx, t->d_small, t->d_gath, 128 * sizeof(float), st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(minmax_ranks_kernel, dim3(1), dim3(64), 0, st, (const float*)t->d_gath, W, D,
+                           t->d_small, t->d_small + 64);
+        ZF_CHECK_LAUNCH("minmax_ranks_kernel");
+      }
       hipLaunchKernelGGL(zf::sb_stats_kernel, dim3(1), dim3(64), 0, st, sb, D, t->d_small, t->d_small + 64,
                          update_stats);
       ZF_CHECK_LAUNCH("sb_stats_kernel");
@@ -1061,19 +1213,22 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
       zf::nsc_dims(t, op, dt, dc, DC, S);
       zf_trainer::NscBufs& nb = t->nsc[i];
       float* bn = nat + op.off_bn;  // [mean, var, scale, bias]
-      if ((long long)B * DC <= zf::kBnSmall) {
+      if (small_ok && (long long)B * DC <= zf::kBnSmall) {
         hipLaunchKernelGGL(zf::bn_fwd_small, dim3(1), dim3(1024), 0, st, sin, c, nb.Uhat, nb.Ubn, bn, nb.mean,
-                           nb.rstd, B, D, C, dt, dc, rot, update_stats);
+                           nb.rstd, B, D, C, dt, dc, rot, lbn.n, lbn.rows, update_stats);
         ZF_CHECK_LAUNCH("bn_fwd_small");
       } else {
         hipLaunchKernelGGL(zf::gather_u_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, sin, c,
                            nb.U, B, D, C, dt, dc, rot);
         ZF_CHECK_LAUNCH("gather_u_kernel");
-        rc = zf_colstats(nb.U, B, DC, DC, 0, nullptr, nullptr, nullptr, nullptr, t->d_dsmall, t->d_dsmall + 128,
-                         t->d_colws, st);
-        if (rc) return rc;
-        hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(128), 0, st, t->d_dsmall, t->d_dsmall + 128, B, DC,
-                           bn, nb.mean, nb.rstd, update_stats);
+        // column sums / sums of squares: leaves -> tree -> (ranks) -> statistics
+        hipLaunchKernelGGL(leaf_colsums_kernel, dim3(blocks_for((int64_t)lbn.n * DC)), dim3(256), 0, st, nb.U,
+                           nullptr, B, DC, lbn.rows, lbn.n, t->d_leaf);
+        ZF_CHECK_LAUNCH("leaf_colsums_kernel");
+        if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st))) return rc;
+        if ((rc = dp_combine(t, t->d_roots, 2 * DC, st))) return rc;
+        hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(64), 0, st, t->d_roots, t->d_roots + DC, Bg, DC, bn,
+                           nb.mean, nb.rstd, update_stats);
         ZF_CHECK_LAUNCH("bn_stats_kernel");
         hipLaunchKernelGGL(zf::bn_apply_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.U,
                            nb.mean, nb.rstd, bn + 2 * DC, bn + 3 * DC, nb.Uhat, nb.Ubn, B, DC);
@@ -1110,17 +1265,21 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
                           ? (float)(-(std::lgamma(desc.latent_param) * 2.0 - std::lgamma(2.0 * desc.latent_param)))
                           : 0.f;
   const float tnm = (float)std::log1p(-2.0 * 0.5 * std::erfc(5.0 / std::sqrt(2.0)));
-  const int nblk = (int)zf::blocks_for(B);
   float* g = t->d_g0;
   float* g_prev = t->d_g1;
-  hipLaunchKernelGGL(zf::latent_loss_kernel, dim3(nblk), dim3(256), 0, st, state(desc.n_ops), t->d_ld, B, D, rot, lt,
-                     a, betac, tnm, g, t->d_part);
+  hipLaunchKernelGGL(zf::latent_loss_kernel, dim3(zf::blocks_for(B)), dim3(256), 0, st, state(desc.n_ops), t->d_ld,
+                     B, Bg, D, rot, lt, a, betac, tnm, g, t->d_rowloss);
   ZF_CHECK_LAUNCH("latent_loss_kernel");
-  hipLaunchKernelGGL(zf::sum_partials_kernel, dim3(1), dim3(64), 0, st, t->d_part, nblk, t->d_part + nblk);
-  ZF_CHECK_LAUNCH("sum_partials_kernel");
+  {
+    const Leaves ll = leaves_for(B, Bg, W, kMaxLeaves);
+    hipLaunchKernelGGL(leaf_sum_kernel, dim3(1), dim3(64), 0, st, t->d_rowloss, B, ll.rows, ll.n, t->d_leaf);
+    ZF_CHECK_LAUNCH("leaf_sum_kernel");
+    if ((rc = launch_tree_cols(t->d_leaf, ll.n, 1, loss_slot(t), st))) return rc;
+    if ((rc = dp_combine(t, loss_slot(t), 1, st))) return rc;
+  }
   // ---- reverse ----
-  ZF_TRY_HIP(hipMemsetAsync(G, 0, (size_t)t->nat_floats * sizeof(float), st));
-  const float gl = -1.0f / (float)B;  // d loss / d log_det of every op and row
+  ZF_TRY_HIP(hipMemsetAsync(G64, 0, (size_t)t->nat_floats * sizeof(double), st));
+  const float gl = -1.0f / (float)Bg;  // d loss / d log_det of every op and row
   for (int i = desc.n_ops - 1; i >= 0; --i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind == ZF_OP_ROLL || op.kind == ZF_OP_SHIFT_BOUNDS) continue;  // Roll: index map; SB: first op
@@ -1142,8 +1301,11 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
     for (int l = op.n_hidden; l >= 0; --l) {
       const int in_w = l == 0 ? DC : op.hidden[l - 1];
       const float* hin = l == 0 ? nb.Ubn : nb.H[l - 1];
-      // dW_l = hin^T . gout ; db_l = colsum(gout)
-      rc = zf::wgrad(in_w, out_w, B, hin, gout, G + op.off_w[l], G + op.off_b[l], t->d_ws, st);
+      // dW_l = hin^T . gout ; db_l = colsum(gout): leaves capped by the
+      // split-K workspace (a power of two, the same on every rank)
+      const int cap = pow2floor(std::min<int64_t>(kMaxLeaves, std::max<int64_t>(1, kWsFloats / ((int64_t)(in_w + 1) * out_w))));
+      rc = zf::wgrad(in_w, out_w, B, leaves_for(B, Bg, W, cap), hin, gout, G64 + op.off_w[l], G64 + op.off_b[l],
+                     t->d_ws, st);
       if (rc) return rc;
       // g_in = gout . W_l^T
       float* gin = l == 0 ? nb.gU : gbufs[which];
@@ -1159,19 +1321,24 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
     }
     // BatchNorm: gU holds d loss / d Ubn
     float* bn = nat + op.off_bn;
-    float* gbn = G + op.off_bn;
-    if ((long long)B * DC <= zf::kBnSmall) {
+    double* gbn = G64 + op.off_bn;
+    if (small_ok && (long long)B * DC <= zf::kBnSmall) {
       hipLaunchKernelGGL(zf::bn_bwd_small, dim3(1), dim3(1024), 0, st, nb.gU, nb.Uhat, bn + 2 * DC, nb.rstd,
-                         gbn + 2 * DC, gbn + 3 * DC, g_prev, B, D, C, dt, dc, r);
+                         gbn + 2 * DC, gbn + 3 * DC, g_prev, B, D, C, dt, dc, r, lbn.n, lbn.rows);
       ZF_CHECK_LAUNCH("bn_bwd_small");
     } else {
-      rc = zf::colsum(nb.gU, nb.Uhat, B, DC, gbn + 2 * DC, t->d_ws, st);
-      if (rc) return rc;
-      rc = zf::colsum(nb.gU, nullptr, B, DC, gbn + 3 * DC, t->d_ws, st);
-      if (rc) return rc;
+      // sums of gUbn and gUbn * Uhat: leaves -> tree (this rank's share of the
+      // scale / bias gradient) -> (ranks) -> the reverse formula's global sums
+      hipLaunchKernelGGL(leaf_colsums_kernel, dim3(blocks_for((int64_t)lbn.n * DC)), dim3(256), 0, st, nb.gU,
+                         nb.Uhat, B, DC, lbn.rows, lbn.n, t->d_leaf);
+      ZF_CHECK_LAUNCH("leaf_colsums_kernel");
+      if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st))) return rc;
+      ZF_TRY_HIP(hipMemcpyAsync(gbn + 3 * DC, t->d_roots, DC * sizeof(double), hipMemcpyDeviceToDevice, st));
+      ZF_TRY_HIP(hipMemcpyAsync(gbn + 2 * DC, t->d_roots + DC, DC * sizeof(double), hipMemcpyDeviceToDevice, st));
+      if ((rc = dp_combine(t, t->d_roots, 2 * DC, st))) return rc;
       // gU := d loss / d U, in place (reads each element before writing it)
       hipLaunchKernelGGL(zf::bn_bwd_kernel, dim3(zf::blocks_for((int64_t)B * DC)), dim3(256), 0, st, nb.gU,
-                         nb.Uhat, bn + 2 * DC, nb.rstd, gbn + 3 * DC, gbn + 2 * DC, nb.gU, B, DC);
+                         nb.Uhat, bn + 2 * DC, nb.rstd, t->d_roots, t->d_roots + DC, nb.gU, B, Bg, DC);
       ZF_CHECK_LAUNCH("bn_bwd_kernel");
       hipLaunchKernelGGL(zf::scatter_gu_kernel, dim3(zf::blocks_for((int64_t)B * dc)), dim3(256), 0, st, nb.gU,
                          g_prev, B, D, C, dt, dc, r);
@@ -1180,6 +1347,18 @@ int trainer_body(zf_trainer_t* t, int B, int update_stats, float* G, hipStream_t
     float* tmp = g;
     g = g_prev;
     g_prev = tmp;
+  }
+  // ---- the gradient: (all ranks' fp64 shares, tree over ranks) -> fp32 ----
+  if (W > 1) {
+    rc = t->comm.allgather(t->comm.ctx, G64, t->d_gath, (size_t)t->nat_floats * sizeof(double), st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(tree_cols_cast_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st,
+                       (const double*)t->d_gath, W, (long long)t->nat_floats, G);
+    ZF_CHECK_LAUNCH("tree_cols_cast_kernel");
+  } else {
+    hipLaunchKernelGGL(cast_f64_f32_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, G64,
+                       (long long)t->nat_floats, G);
+    ZF_CHECK_LAUNCH("cast_f64_f32_kernel");
   }
   return ZF_OK;
 }
@@ -1209,7 +1388,7 @@ int step_graph(zf_trainer_t* t, int B, hipGraphExec_t* out) {
     t->graphs.clear();
   }
   ZF_TRY_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
-  int rc = trainer_body(t, B, 1, t->d_grad, t->cap);
+  int rc = trainer_body(t, B, B, 1, t->d_grad, t->cap);
   if (!rc) rc = trainer_update(t, t->cap);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(t->cap, &g);
@@ -1231,34 +1410,50 @@ int step_graph(zf_trainer_t* t, int B, hipGraphExec_t* out) {
 
 extern "C" {
 
-int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_t B, int update_stats,
-                         double* loss, float* grad, void* stream) {
+int zf_trainer_loss_grad_shard(zf_trainer_t* t, const float* x, const float* c, int64_t rows, int64_t global_rows,
+                               int update_stats, double* loss, float* grad, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int rc = zf::trainer_stage(t, x, c, B, st);
+  int rc = zf::trainer_stage(t, x, c, rows, st);
   if (rc) return rc;
-  rc = zf::trainer_body(t, (int)B, update_stats, grad ? grad : t->d_grad, st);
+  if (global_rows < rows || (t->comm.world == 1 && global_rows != rows))
+    return zf::einval("global_rows %lld vs rows %lld (world %d)", (long long)global_rows, (long long)rows, t->comm.world);
+  rc = zf::trainer_body(t, (int)rows, global_rows, update_stats, grad ? grad : t->d_grad, st);
   if (rc) return rc;
-  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t, (int)B), sizeof(double), hipMemcpyDeviceToDevice, st));
+  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t), sizeof(double), hipMemcpyDeviceToDevice, st));
   return ZF_OK;
 }
 
-int zf_trainer_step(zf_trainer_t* t, const float* x, const float* c, int64_t B, double* loss, void* stream) {
+int zf_trainer_loss_grad(zf_trainer_t* t, const float* x, const float* c, int64_t B, int update_stats,
+                         double* loss, float* grad, void* stream) {
+  if (!t) return zf::einval("trainer is NULL");
+  return zf_trainer_loss_grad_shard(t, x, c, B, B * t->comm.world, update_stats, loss, grad, stream);
+}
+
+int zf_trainer_step_shard(zf_trainer_t* t, const float* x, const float* c, int64_t rows, int64_t global_rows,
+                          double* loss, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int rc = zf::trainer_stage(t, x, c, B, st);
+  int rc = zf::trainer_stage(t, x, c, rows, st);
   if (rc) return rc;
-  if (t->use_graph) {
+  if (global_rows < rows || (t->comm.world == 1 && global_rows != rows))
+    return zf::einval("global_rows %lld vs rows %lld (world %d)", (long long)global_rows, (long long)rows, t->comm.world);
+  if (t->use_graph && t->comm.world == 1) {  // collectives are issued eagerly
     hipGraphExec_t exec = nullptr;
-    rc = zf::step_graph(t, (int)B, &exec);
+    rc = zf::step_graph(t, (int)rows, &exec);
     if (rc) return rc;
     ZF_TRY_HIP(hipGraphLaunch(exec, st));
   } else {
-    rc = zf::trainer_body(t, (int)B, 1, t->d_grad, st);
+    rc = zf::trainer_body(t, (int)rows, global_rows, 1, t->d_grad, st);
     if (!rc) rc = zf::trainer_update(t, st);
     if (rc) return rc;
   }
   t->t += 1;
-  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t, (int)B), sizeof(double), hipMemcpyDeviceToDevice, st));
+  if (loss) ZF_TRY_HIP(hipMemcpyAsync(loss, zf::loss_slot(t), sizeof(double), hipMemcpyDeviceToDevice, st));
   return ZF_OK;
+}
+
+int zf_trainer_step(zf_trainer_t* t, const float* x, const float* c, int64_t B, double* loss, void* stream) {
+  if (!t) return zf::einval("trainer is NULL");
+  return zf_trainer_step_shard(t, x, c, B, B * t->comm.world, loss, stream);
 }
 
 int zf_trainer_get_blob(zf_trainer_t* t, float* blob_host) {

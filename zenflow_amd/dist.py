@@ -1,5 +1,10 @@
-"""Data-parallel log_prob across GPUs: one process per GPU, contiguous batch
-shards, and a single all-reduce of the fp64 NLL partial sum.
+"""Data parallelism across GPUs, one process per GPU.
+
+log_prob: contiguous batch shards and a single all-reduce of the fp64 NLL
+partial sum.  Training: the trainer's all-gather at every
+batch reduction (``RcclCommunicator.trainer_comm_desc`` / ``HostAllgather``;
+zf_trainer_set_comm), with the leaf-tree schedule mirrored on the host by
+``reduction_leaves`` / ``tree_sum``.
 
 log_prob is a per-sample map in eval mode (BatchNorm running stats,
 ShiftBounds stored min/max), so the only exchange is the scalar
@@ -62,10 +67,91 @@ class RcclCommunicator:
             L.stream() if stream is None else stream), "allreduce")
         return buf
 
+    def trainer_comm_desc(self) -> L.ZfCommDesc:
+        """zf_comm_desc for data-parallel training (zf_trainer_set_comm):
+        the trainer's all-gather is ncclAllGather on this communicator."""
+        fn = C.cast(L.load_library().zf_rccl_allgather, C.c_void_p).value
+        return L.ZfCommDesc(self.rank, self.world, self.comm, fn)
+
     def close(self):
         if self.comm:
             L.load_library().zf_rccl_comm_destroy(self.comm)
             self.comm = None
+
+
+class HostAllgather:
+    """zf_allgather_fn over the control-plane rendezvous (device -> host ->
+    rank-order gather -> device, synchronous on the trainer's stream).  For
+    data-parallel training where RCCL cannot run: several ranks sharing one
+    GPU (the multi-process GPU tests; RCCL refuses two ranks on one device).
+    The data path of a real multi-GPU job is ``RcclCommunicator``."""
+
+    def __init__(self, rdzv):
+        self.rdzv = rdzv
+        self.rank, self.world = rdzv.rank, rdzv.world
+        self._cb = L.ALLGATHER_FN(self._allgather)  # kept alive with this object
+
+    def _allgather(self, ctx, send, recv, nbytes, stream) -> int:
+        try:
+            lib = L.load_library()
+            buf = C.create_string_buffer(max(1, nbytes))
+            check(lib.zf_stream_synchronize(stream), "allgather sync")
+            check(lib.zf_memcpy_dtoh(buf, send, nbytes, stream), "allgather dtoh")
+            check(lib.zf_stream_synchronize(stream), "allgather sync")
+            out = b"".join(self.rdzv.allgather_bytes(buf.raw[:nbytes], "trainer_ag"))
+            check(lib.zf_memcpy_htod(recv, out, len(out), stream), "allgather htod")
+            check(lib.zf_stream_synchronize(stream), "allgather sync")
+            return 0
+        except Exception as e:  # a C caller: report, do not unwind through ctypes
+            import sys
+
+            print(f"HostAllgather rank {self.rank}: {e!r}", file=sys.stderr, flush=True)
+            return 1
+
+    def trainer_comm_desc(self) -> L.ZfCommDesc:
+        return L.ZfCommDesc(self.rank, self.world, None, C.cast(self._cb, C.c_void_p).value)
+
+    def close(self):
+        pass
+
+
+def reduction_leaves(rows: int, global_rows: int, world: int, cap: int = 64) -> Tuple[int, int]:
+    """(leaves on this rank, rows per leaf) of every batch reduction of the
+    trainer — the host mirror of zf_train.hip ``leaves_for``: ~32 rows per
+    leaf, at most ``cap`` (a power of two) leaves in the global batch, a
+    power of two per rank."""
+    want = max(1, min(int(global_rows) // 32, int(cap)))
+    per = max(1, want // max(1, int(world)))
+    n = 1 << (per.bit_length() - 1)
+    return n, (int(rows) + n - 1) // n
+
+
+def tree_sum(leaves: np.ndarray) -> np.ndarray:
+    """The trainer's pairwise leaf tree (zf_train.hip ``tree_n``) in fp64 over
+    axis 0: level s adds element i + s into i for i a multiple of 2s."""
+    v = [np.asarray(x, np.float64) for x in leaves]
+    n = len(v)
+    s = 1
+    while s < n:
+        for i in range(0, n, 2 * s):
+            if i + s < n:
+                v[i] = v[i] + v[i + s]
+        s *= 2
+    return v[0]
+
+
+def leaf_tree_colsum(x: np.ndarray, global_rows: int, world: int, cap: int = 64) -> np.ndarray:
+    """This rank's subtree root of the column sums of ``x`` (rows x cols,
+    fp32): leaves of ``reduction_leaves`` rows summed in row order in fp64,
+    then ``tree_sum`` — the schedule of the trainer's BatchNorm sums."""
+    n, rows = reduction_leaves(x.shape[0], global_rows, world, cap)
+    parts = []
+    for z in range(n):
+        acc = np.zeros(x.shape[1:], np.float64)
+        for b in range(min(x.shape[0], z * rows), min(x.shape[0], (z + 1) * rows)):
+            acc = acc + x[b].astype(np.float64)
+        parts.append(acc)
+    return tree_sum(parts)
 
 
 class HostCommunicator:

@@ -132,6 +132,12 @@ class FileRendezvous:
         self._write(f"{t}.{self.rank}", json.dumps(value).encode())
         return [json.loads(self._wait(f"{t}.{r}")) for r in range(self.world)]
 
+    def allgather_bytes(self, data: bytes, tag: Optional[str] = None) -> List[bytes]:
+        """Every rank's ``data`` (raw bytes), in rank order."""
+        t = self._tag(tag)
+        self._write(f"{t}.{self.rank}", bytes(data))
+        return [self._wait(f"{t}.{r}") for r in range(self.world)]
+
     def broadcast_bytes(self, data: Optional[bytes], src: int = 0, tag: Optional[str] = None) -> bytes:
         t = self._tag(tag)
         if self.rank == src:

@@ -27,6 +27,7 @@ import numpy as np
 
 from . import _lib as L
 from ._lib import DeviceArray, check
+from .dist import shard_rows
 from .random import PRNGKey
 
 
@@ -65,7 +66,11 @@ class Trainer:
     batches of up to ``batch_max`` rows."""
 
     def __init__(self, flow, variables: Dict[str, Any], D: int, C: int, batch_max: int,
-                 optimizer: Optional[Optimizer] = None):
+                 optimizer: Optional[Optimizer] = None, comm=None):
+        """``comm``: data parallelism — an object with ``rank``, ``world`` and
+        ``trainer_comm_desc()`` (``dist.RcclCommunicator``, or
+        ``dist.HostAllgather`` for ranks sharing a GPU); each rank then passes
+        its shard of every global batch."""
         L.ensure_device()
         self.flow = flow
         self.D, self.C = int(D), int(C)
@@ -80,6 +85,12 @@ class Trainer:
             self.batch_max, ct.byref(opt), ct.byref(h)), "zf_trainer_create")
         self.handle = h.value
         self._loss = DeviceArray((1,), np.float64)
+        self.comm = comm
+        self.world = 1
+        if comm is not None and comm.world > 1:
+            self._comm_desc = comm.trainer_comm_desc()  # kept alive: the C side holds its pointers
+            check(L.load_library().zf_trainer_set_comm(self.handle, ct.byref(self._comm_desc)), "zf_trainer_set_comm")
+            self.world = comm.world
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -97,27 +108,33 @@ class Trainer:
             a = a.reshape(-1, 1)
         return DeviceArray.from_numpy(np.ascontiguousarray(a))
 
-    def loss_grad(self, x, c=None, update_stats: bool = False) -> Tuple[float, np.ndarray]:
-        """(loss, gradient in the natural blob layout) — loss_fn + jax.grad."""
+    def _global(self, rows: int, global_rows: Optional[int]) -> int:
+        return int(global_rows) if global_rows is not None else int(rows) * self.world
+
+    def loss_grad(self, x, c=None, update_stats: bool = False,
+                  global_rows: Optional[int] = None) -> Tuple[float, np.ndarray]:
+        """(loss, gradient in the natural blob layout) — loss_fn + jax.grad.
+        Data parallel: ``x`` is this rank's shard of a global batch of
+        ``global_rows`` rows (default: equal shards); both results are global."""
         xd, cd = self._dev(x, self.D), self._dev(c, self.C)
         g = DeviceArray((self.program.blob.size,))
-        check(L.load_library().zf_trainer_loss_grad(
-            self.handle, xd.ptr, None if cd is None else cd.ptr, xd.shape[0], 1 if update_stats else 0,
-            self._loss.ptr, g.ptr, L.stream()), "zf_trainer_loss_grad")
+        check(L.load_library().zf_trainer_loss_grad_shard(
+            self.handle, xd.ptr, None if cd is None else cd.ptr, xd.shape[0], self._global(xd.shape[0], global_rows),
+            1 if update_stats else 0, self._loss.ptr, g.ptr, L.stream()), "zf_trainer_loss_grad")
         return float(self._loss.numpy()[0]), g.numpy()
 
     def grad_tree(self, grad_blob: np.ndarray) -> Dict[str, Any]:
         """Gradient blob -> FLAX ``params`` tree (like jax.grad's output)."""
         return {"bijector": self.program.blob_to_variables(grad_blob)["params"]}
 
-    def step(self, x, c=None) -> None:
+    def step(self, x, c=None, global_rows: Optional[int] = None) -> None:
         xd, cd = self._dev(x, self.D), self._dev(c, self.C)
-        self._step_rows(xd.ptr, None if cd is None else cd.ptr, xd.shape[0])
+        self._step_rows(xd.ptr, None if cd is None else cd.ptr, xd.shape[0], global_rows)
 
-    def _step_rows(self, xptr: int, cptr: Optional[int], rows: int) -> None:
+    def _step_rows(self, xptr: int, cptr: Optional[int], rows: int, global_rows: Optional[int] = None) -> None:
         """One step on ``rows`` device-resident rows (raw pointers; async)."""
-        check(L.load_library().zf_trainer_step(self.handle, xptr, cptr, rows, self._loss.ptr, L.stream()),
-              "zf_trainer_step")
+        check(L.load_library().zf_trainer_step_shard(self.handle, xptr, cptr, rows, self._global(rows, global_rows),
+                                                     self._loss.ptr, L.stream()), "zf_trainer_step")
 
     def last_loss(self) -> float:
         return float(self._loss.numpy()[0])
@@ -152,12 +169,19 @@ def train(
     seed: int = 0,
     progress: bool = True,
     initial_variables=None,
+    comm=None,
 ) -> Tuple[Dict[str, Any], int, List[float], List[float]]:
     """Trains the normalizing flow on the provided inputs (train.py:18-138).
 
     Same arguments, defaults, early stopping and return value
     ``(best_variables, best_epoch, loss_train, loss_test)`` as the reference;
-    ``optimizer`` is an :class:`Optimizer` (``nadamw(...)`` / ``adamw(...)``)."""
+    ``optimizer`` is an :class:`Optimizer` (``nadamw(...)`` / ``adamw(...)``).
+
+    ``comm`` (data parallelism, one process per GPU, every rank calling with
+    the same data and seed): each global batch of ``batch_size`` rows is cut
+    into contiguous per-rank shards (``dist.shard_rows``); the trainer's
+    reductions make every rank's parameters identical after every step.  A
+    batch with fewer rows than ranks is skipped."""
     if warmup < 1:
         warmup = warmup * epochs
     warmup = int(warmup)
@@ -180,7 +204,10 @@ def train(
         variables = initial_variables
     D = X_train.shape[1]
     Cd = 0 if C_train is None else C_train.shape[1]
-    trainer = Trainer(flow, variables, D, Cd, min(batch_size, X_train.shape[0]), optimizer)
+    world = 1 if comm is None else int(comm.world)
+    rank = 0 if comm is None else int(comm.rank)
+    shard_max = -(-min(batch_size, X_train.shape[0]) // world)
+    trainer = Trainer(flow, variables, D, Cd, shard_max, optimizer, comm=comm)
 
     loop = range(epochs)
     if progress:
@@ -206,8 +233,11 @@ def train(
         C_dev = None if C_perm is None else DeviceArray.from_numpy(C_perm)
         for batch_idx in range(0, n, batch_size):
             rows = min(batch_size, n - batch_idx)
-            trainer._step_rows(X_dev.ptr + batch_idx * D * 4,
-                               None if C_dev is None else C_dev.ptr + batch_idx * Cd * 4, rows)
+            if rows < world:
+                continue
+            lo, hi = shard_rows(rows, rank, world)
+            trainer._step_rows(X_dev.ptr + (batch_idx + lo) * D * 4,
+                               None if C_dev is None else C_dev.ptr + (batch_idx + lo) * Cd * 4, hi - lo, rows)
         X = X_perm[batch_idx : batch_idx + batch_size]
         C = None if C_perm is None else C_perm[batch_idx : batch_idx + batch_size]
 
