@@ -1,0 +1,54 @@
+"""Stall / co-execution counters of the headline kernel (scripts/pmc_stall.sh
+passes in gpurun_out/pmc_st*) -> profiles/<tag>_x3_stall_counters.json.
+
+Derived (per launch of the 2^20-row grid; the kernel's cycles =
+GRBM_GUI_ACTIVE / 8 XCDs; SIMD-cycle counters are summed over 1024 SIMDs;
+SQ_WAVE_CYCLES / SQ_ACTIVE_* / SQ_WAIT_* are wave quad-cycles):
+  mfma_busy     SQ_VALU_MFMA_BUSY_CYCLES / (1024 cycles)
+  coexec        SQ_VALU_MFMA_COEXEC_CYCLES / (1024 cycles)  (VALU and MFMA at once)
+  valu_issue    4 SQ_ACTIVE_INST_VALU / (1024 cycles)       (MFMA issue included)
+  wave split    SQ_ACTIVE_INST_ANY / SQ_WAIT_INST_ANY / SQ_WAIT_ANY over SQ_WAVE_CYCLES"""
+import csv
+import glob
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def main(tag="r02", src=ROOT / "gpurun_out"):
+    agg = {}
+    for path in glob.glob(str(Path(src) / "pmc_st*" / "run_counter_collection.csv")):
+        for r in csv.DictReader(open(path)):
+            if "flow_kernel_x3" not in r["Kernel_Name"]:
+                continue
+            if int(r.get("Grid_Size") or r["Grid_Size_X"]) < (1 << 20):
+                continue
+            agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
+    cyc = med["GRBM_GUI_ACTIVE"] / 8
+    simd = 1024 * cyc
+    waves = med["SQ_WAVE_CYCLES"]
+    out = {
+        "kernel": "flow_kernel_x3<2,16,4,false,false,false> (cfg2), grid 2^20 rows",
+        "counters_median": med,
+        "kernel_cycles": cyc,
+        "mfma_busy": med["SQ_VALU_MFMA_BUSY_CYCLES"] / simd,
+        "valu_mfma_coexec": med["SQ_VALU_MFMA_COEXEC_CYCLES"] / simd,
+        "valu_issue": 4 * med["SQ_ACTIVE_INST_VALU"] / simd,
+        "wave_active": med["SQ_ACTIVE_INST_ANY"] / waves,
+        "wave_wait_inst_any": med["SQ_WAIT_INST_ANY"] / waves,
+        "wave_wait_any": med["SQ_WAIT_ANY"] / waves,
+        "per_wave_coupling": {k: med[c] / 32768 / 4 for k, c in (
+            ("valu_insts", "SQ_INSTS_VALU"), ("mfma_insts", "SQ_INSTS_MFMA"), ("trans_f32_insts", "SQ_INSTS_VALU_TRANS_F32"),
+            ("salu_insts", "SQ_INSTS_SALU"), ("lds_insts", "SQ_INSTS_LDS"), ("branches", "SQ_INSTS_BRANCH"))},
+        "lds_bank_conflicts": med.get("SQ_LDS_BANK_CONFLICT"),
+    }
+    out["simd_idle"] = 1 - out["mfma_busy"] - out["valu_issue"] + out["valu_mfma_coexec"]
+    (ROOT / "profiles" / f"{tag}_x3_stall_counters.json").write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps({k: v for k, v in out.items() if k != "counters_median"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

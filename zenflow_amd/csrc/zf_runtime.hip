@@ -44,7 +44,12 @@ int zf_device_name(int device, char* buf, int buflen) {
   if (!buf || buflen <= 0) return zf::einval("bad buffer");
   hipDeviceProp_t p;
   ZF_TRY_HIP(hipGetDeviceProperties(&p, device));
-  snprintf(buf, buflen, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+  // p.name is the marketing name from libdrm's amdgpu.ids; boxes without that
+  // file report "": fall back to the PCI device id
+  char name[64];
+  if (p.name[0]) snprintf(name, sizeof(name), "%s", p.name);
+  else snprintf(name, sizeof(name), "AMD GPU [1002:%04x]", (unsigned)p.pciDeviceID);
+  snprintf(buf, buflen, "%s (%s, %d CUs)", name, p.gcnArchName, p.multiProcessorCount);
   return ZF_OK;
 }
 

@@ -2,9 +2,10 @@
 (reference: src/zenflow/distributions.py).
 
 ``log_prob`` runs on the GPU (the same latent epilogue the fused flow kernel
-uses).  ``sample`` draws on the host from a seeded numpy Generator: JAX's
-threefry stream is not reproducible without JAX, so sampling parity is
-statistical (moments), exactly as the reference tests check it."""
+uses).  ``sample`` draws on the GPU too (``zf_latent_sample``: Philox4x32-10
+keyed by the seed, counter = (row, dim), zf_random.h): JAX's threefry stream
+is not reproducible without JAX, so sampling parity is statistical (KS tests,
+moments), as the reference tests check it."""
 
 from __future__ import annotations
 
