@@ -43,6 +43,9 @@ PEAK_HBM_GBS = 8000.0
 
 WORKLOADS = {
     # name: (D, C, K, layers, couplings, latent, mode)
+    # cfg1: two_moons through the drop-in API (host arrays in and out, the
+    # FLAX-style apply of examples/two_moons.ipynb), batch 4096
+    "cfg1": (2, 0, 8, (128, 128), 2, "beta", "apply"),
     "cfg2": (4, 0, 16, (128, 128), 4, "normal", "log_prob"),
     "cfg3": (4, 0, 16, (128, 128), 4, "normal", "inverse"),
     "cfg3s": (4, 0, 16, (128, 128), 4, "normal", "sample"),  # Flow.sample, latent drawn on device
@@ -208,7 +211,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--rows-log2", type=int, default=20, help="rows per GPU = 2^k")
+    ap.add_argument("--rows-log2", type=int, default=None, help="rows per GPU = 2^k (default 20; cfg1: 12)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-spline-kernel", action="store_true")
@@ -246,7 +249,7 @@ def main():
     L.ensure_device()
     name = args.config
     D, C, K, layers, nL, latent, mode = WORKLOADS[name]
-    N = 1 << args.rows_log2
+    N = 1 << (args.rows_log2 if args.rows_log2 is not None else (12 if mode == "apply" else 20))
     flow = build_model(name)
     # Random-init weights of the named architecture (flax default initialisers),
     # then one train-mode pass over a separate 2^16 batch to set the ShiftBounds
@@ -277,6 +280,12 @@ def main():
     def step(ev=None):
         if mode == "log_prob":
             dp.step(xd, cd, out, ev)
+        elif mode == "apply":  # Flow.__call__ through apply: host x in, host log_prob out
+            if ev is not None:
+                ev[0].record()
+            flow.apply(variables, x, c)
+            if ev is not None:
+                ev[1].record()
         elif mode == "sample":
             if ev is not None:
                 ev[0].record()
@@ -323,7 +332,8 @@ def main():
     traffic = pmc.get("hbm_bytes_per_launch")
     result = {
         "metric": "log_prob samples/sec (+ NLL match) 4D 16-knot 4-layer flow, batch 2^20"
-        if name == "cfg2" else f"{mode} samples/sec ({name})",
+        if name == "cfg2" else ("log_prob samples/sec through Flow.apply (host in/out)" if mode == "apply"
+                                else f"{mode} samples/sec ({name})"),
         "value": value,
         "unit": "samples/s",
         "n_gpus": world,
@@ -365,13 +375,35 @@ def main():
     if mode == "log_prob":
         result["nll"] = dp.nll(N * world)
         result["config"]["communicator_ranks"] = comm.world if comm is not None else 1
+    if mode == "apply":
+        # the same batch resident in HBM (fused kernel + NLL reduce only), and
+        # Flow.sample through apply (latent drawn on the device, host out)
+        rate = {}
+        res_out = DeviceArray((N,))
+        for tag in ("log_prob_resident_hbm", "sample_apply"):
+            def one():
+                if tag == "sample_apply":
+                    flow.apply(variables, N, method="sample", seed=7)
+                else:
+                    dp.step(xd, cd, res_out)
+            for _ in range(3):
+                one()
+            sync_all()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                one()
+            sync_all()
+            rate[tag] = N * args.steps / (time.perf_counter() - t0)
+        result["apply_path"] = {"log_prob_apply_samples_per_s": value, **{k + "_samples_per_s": v for k, v in rate.items()},
+                                "note": "value = Flow.apply(variables, x_host) per step: host->device copy, fused "
+                                        "kernel, device->host copy and Python dispatch; cached device program"}
     if not args.no_spline_kernel and rank == 0:
         result["spline_kernel"] = spline_kernel_roofline(N, 2, K, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         spec = oracle_spec(name)
-        if mode == "log_prob":
+        if mode in ("log_prob", "apply"):
             cb, outs = cpu_baseline(spec, variables, x, c, args.cpu_budget)
-            lp = out.numpy()
+            lp = out.numpy() if mode == "log_prob" else flow.apply(variables, x, c)
             errs, mism = [], 0
             for lo, ref in outs:
                 g = lp[lo : lo + ref.shape[0]]

@@ -83,6 +83,8 @@ def main(mode, outdir):
         res["sum"] = tree_sum(parts).tobytes().hex()
     elif mode == "train_dp":
         _train_dp(rdzv, res, outdir)
+    elif mode == "train_fn":
+        _train_fn(rdzv, res, outdir)
     rdzv.close()
     Path(outdir, f"rank{rank}.json").write_text(json.dumps(res))
 
@@ -117,6 +119,36 @@ def _train_dp(rdzv, res, outdir):
     np.savez(Path(outdir, f"rank{rdzv.rank}.npz"), grad=g, loss=np.float64(loss), blob=blob,
              last_loss=np.float64(tr.last_loss()))
     res["rows"] = b - a
+
+
+
+def two_moons_flow():
+    import zenflow_amd as zf
+    from zenflow_amd import bijectors as bi
+    from zenflow_amd import distributions as dist
+
+    return zf.Flow(bi.rolling_spline_coupling(2, knots=8, layers=(64, 64)), latent=dist.Beta())
+
+
+def two_moons_data():
+    from sklearn.datasets import make_moons
+
+    X, _ = make_moons(3000, noise=0.05, random_state=2)
+    return X.astype(np.float32)
+
+
+def _train_fn(rdzv, res, outdir):
+    """zenflow_amd.train(..., comm=HostAllgather) on every rank: the same
+    data and seed, each rank stepping on its shard of every batch."""
+    import zenflow_amd as zf
+    from zenflow_amd.dist import HostAllgather
+    from zenflow_amd.io import flatten_variables
+
+    X = two_moons_data()
+    best, best_epoch, lt, ls = zf.train(two_moons_flow(), X[:2400], X[2400:], epochs=int(os.environ.get("ZF_TEST_EPOCHS", "20")),
+                                        batch_size=512, progress=False, comm=HostAllgather(rdzv))
+    np.savez(Path(outdir, f"rank{rdzv.rank}.npz"), best_epoch=best_epoch, lt=np.asarray(lt), ls=np.asarray(ls),
+             **{"v:" + k: v for k, v in flatten_variables(best).items()})
 
 
 if __name__ == "__main__":

@@ -43,3 +43,27 @@ def test_two_ranks_match_one_device_bitwise(tmp_path, name, N, seed):
         assert np.array_equal(r["grad"], g), f"rank {k}: {np.sum(r['grad'] != g)} gradient entries differ"
         assert float(r["last_loss"]) == tr.last_loss(), f"rank {k} last loss"
         assert np.array_equal(r["blob"], blob, equal_nan=True), f"rank {k}: {np.sum(r['blob'] != blob)} blob entries"
+
+
+def test_train_function_two_ranks_match_one_device(tmp_path):
+    """zenflow_amd.train(..., comm=...) (train.py:18-138's loop, batches cut
+    into per-rank shards; 2400 rows in batches of 512, the last one ragged):
+    both ranks return the one-device result — the same losses per epoch, the
+    same best epoch and the same best variables, bit for bit."""
+    import zenflow_amd as zf
+    from tests.dist_worker import two_moons_data, two_moons_flow
+    from zenflow_amd.io import flatten_variables
+    from zenflow_amd.launch import spawn
+
+    env = dict(os.environ, ZF_TEST_EPOCHS="20")
+    assert spawn(2, [WORKER, "train_fn", str(tmp_path)], env=env, timeout=300) == 0
+    X = two_moons_data()
+    best, best_epoch, lt, ls = zf.train(two_moons_flow(), X[:2400], X[2400:], epochs=20, batch_size=512,
+                                        progress=False)
+    flat = flatten_variables(best)
+    for k in range(2):
+        r = np.load(tmp_path / f"rank{k}.npz")
+        assert int(r["best_epoch"]) == best_epoch
+        assert np.array_equal(r["lt"], np.asarray(lt)) and np.array_equal(r["ls"], np.asarray(ls))
+        for name, v in flat.items():
+            assert np.array_equal(r["v:" + name], v), f"rank {k}: {name}"

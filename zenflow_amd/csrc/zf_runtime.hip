@@ -45,10 +45,10 @@ int zf_device_name(int device, char* buf, int buflen) {
   hipDeviceProp_t p;
   ZF_TRY_HIP(hipGetDeviceProperties(&p, device));
   // p.name is the marketing name from libdrm's amdgpu.ids; boxes without that
-  // file report "": fall back to the PCI device id
+  // file report "": a generic name (the arch string follows)
   char name[64];
   if (p.name[0]) snprintf(name, sizeof(name), "%s", p.name);
-  else snprintf(name, sizeof(name), "AMD GPU [1002:%04x]", (unsigned)p.pciDeviceID);
+  else snprintf(name, sizeof(name), "AMD GPU");
   snprintf(buf, buflen, "%s (%s, %d CUs)", name, p.gcnArchName, p.multiProcessorCount);
   return ZF_OK;
 }
