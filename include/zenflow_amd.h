@@ -102,8 +102,19 @@ int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, in
 #define ZF_LATENT_TRUNCNORM 3 /* distributions.py:65-78  */
 #define ZF_LATENT_UNIFORM 4   /* distributions.py:119-126 */
 
-/* Activation of the conditioner's hidden layers (NSC.act, bijectors.py:319). */
-#define ZF_ACT_SWISH 0
+/* Activation of the conditioner's hidden layers (NSC.act, bijectors.py:319;
+ * the flax.linen / jax.nn functions of those names).  The split-MFMA kernel
+ * implements swish (the reference default); the others run on the fp32
+ * kernel and in the trainer. */
+#define ZF_ACT_SWISH 0      /* nn.swish = nn.silu: x * sigmoid(x) */
+#define ZF_ACT_RELU 1       /* nn.relu */
+#define ZF_ACT_TANH 2       /* nn.tanh */
+#define ZF_ACT_SIGMOID 3    /* nn.sigmoid */
+#define ZF_ACT_GELU 4       /* nn.gelu (approximate=True, the flax default) */
+#define ZF_ACT_SOFTPLUS 5   /* nn.softplus = logaddexp(x, 0) */
+#define ZF_ACT_ELU 6        /* nn.elu (alpha 1) */
+#define ZF_ACT_LEAKY_RELU 7 /* nn.leaky_relu (negative slope 0.01) */
+#define ZF_ACT_COUNT 8
 
 /* ShiftBounds per-dim modes (bijectors.py:183-205). */
 #define ZF_SB_NONE 0  /* unbounded: running min/max affine + clip        */

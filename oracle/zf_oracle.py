@@ -397,6 +397,31 @@ def swish(x):
         return x * (np.asarray(1, x.dtype) / (np.asarray(1, x.dtype) + np.exp(-x)))
 
 
+def activation(name, x):
+    """The conditioner activation (bijectors.py:319 ``act``, default
+    flax.linen.swish) in the dtype of ``x``: the jax.nn definitions."""
+    dt = x.dtype
+    with np.errstate(all="ignore"):
+        if name in ("swish", "silu"):
+            return swish(x)
+        if name == "relu":
+            return np.maximum(x, _c(dt, 0))
+        if name == "tanh":
+            return np.tanh(x)
+        if name == "sigmoid":
+            return _c(dt, 1) / (_c(dt, 1) + np.exp(-x))
+        if name == "gelu":  # approximate=True (flax.linen.gelu default)
+            c = _c(dt, np.sqrt(2 / np.pi))
+            return _c(dt, 0.5) * x * (_c(dt, 1) + np.tanh(c * (x + _c(dt, 0.044715) * x * x * x)))
+        if name == "softplus":
+            return np.logaddexp(x, _c(dt, 0))
+        if name == "elu":
+            return np.where(x > 0, x, np.expm1(np.minimum(x, _c(dt, 0))))
+        if name == "leaky_relu":
+            return np.where(x >= 0, x, _c(dt, 0.01) * x)
+    raise ValueError(name)
+
+
 def _batchnorm(u, p, s, train, dt, momentum=0.99, eps=1e-5):
     """flax.linen.BatchNorm (bijectors.py:342): y = (u-mean)*rsqrt(var+eps)*scale+bias."""
     if train:
@@ -431,7 +456,7 @@ def nsc_params(spec, params, stats, x, c, train, dt):
     nl = len(spec.get("layers", (128, 128)))
     for li in range(nl):  # :343-345
         d = params[f"Dense_{li}"]
-        u = _perturb(swish(u @ np.asarray(d["kernel"], dt) + np.asarray(d["bias"], dt)))
+        u = _perturb(activation(spec.get("act", "swish"), u @ np.asarray(d["kernel"], dt) + np.asarray(d["bias"], dt)))
     d = params[f"Dense_{nl}"]
     p = _perturb(u @ np.asarray(d["kernel"], dt) + np.asarray(d["bias"], dt))  # :346
     p = p.reshape((x.shape[0], split, S))  # :347

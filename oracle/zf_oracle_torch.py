@@ -122,8 +122,25 @@ def shift_bounds(spec, st, x):
     return torch.stack(cols, dim=1), ld
 
 
-def _swish(x):
-    return x * torch.sigmoid(x)
+def _act(name, x):
+    """bijectors.py:319 ``act`` (jax.nn definitions; as zf_oracle.activation)."""
+    if name in ("swish", "silu"):
+        return x * torch.sigmoid(x)
+    if name == "relu":
+        return torch.clamp(x, min=0)
+    if name == "tanh":
+        return torch.tanh(x)
+    if name == "sigmoid":
+        return torch.sigmoid(x)
+    if name == "gelu":
+        return 0.5 * x * (1 + torch.tanh(math.sqrt(2 / math.pi) * (x + 0.044715 * x * x * x)))
+    if name == "softplus":
+        return torch.logaddexp(x, torch.zeros_like(x))
+    if name == "elu":
+        return torch.where(x > 0, x, torch.expm1(torch.clamp(x, max=0)))
+    if name == "leaky_relu":
+        return torch.where(x >= 0, x, 0.01 * x)
+    raise ValueError(name)
 
 
 def nsc(spec, p, x, c):
@@ -140,7 +157,7 @@ def nsc(spec, p, x, c):
     nl = len(spec.get("layers", (128, 128)))
     for li in range(nl):
         d = p[f"Dense_{li}"]
-        u = _swish(u @ d["kernel"] + d["bias"])
+        u = _act(spec.get("act", "swish"), u @ d["kernel"] + d["bias"])
     d = p[f"Dense_{nl}"]
     q = (u @ d["kernel"] + d["bias"]).reshape(x.shape[0], dt_, 3 * K - 1)
     dx = _softmax_with_threshold(q[..., :K], EPS)

@@ -36,7 +36,17 @@ CONFIGS = {
     "d3k32": dict(D=3, C=0, K=32, layers=(128, 96), latent="beta"),
     "d4h256k8": dict(D=4, C=1, K=8, layers=(256, 256), latent="normal"),
     "d5h64": dict(D=5, C=0, K=16, layers=(64, 64), latent="normal"),
+    # NeuralSplineCoupling(act=...) other than swish (bijectors.py:319): the
+    # fp32 kernel and the trainer
+    "relu": dict(D=4, C=0, K=16, layers=(128, 128), latent="normal", act="relu"),
+    "gelu": dict(D=3, C=1, K=8, layers=(64, 64), latent="beta", act="gelu"),
+    "tanh": dict(D=2, C=0, K=16, layers=(128,), latent="normal", act="tanh"),
+    "softplus": dict(D=4, C=0, K=8, layers=(32, 32), latent="normal", act="softplus"),
+    "sigmoid": dict(D=2, C=2, K=16, layers=(64,), latent="beta", act="sigmoid"),
+    "elu": dict(D=5, C=0, K=8, layers=(64, 64), latent="normal", act="elu"),
+    "leaky_relu": dict(D=4, C=0, K=16, layers=(96,), latent="normal", act="leaky_relu"),
 }
+ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu"]
 
 
 def chain_spec(cfg):
@@ -44,9 +54,9 @@ def chain_spec(cfg):
     L = cfg.get("couplings", D)
     bij = [{"type": "shift_bounds", "margin": cfg.get("margin", 0.1), "bounds": cfg.get("bounds", ())}]
     for _ in range(L - 1):
-        bij.append({"type": "nsc", "knots": K, "layers": layers})
+        bij.append({"type": "nsc", "knots": K, "layers": layers, "act": cfg.get("act", "swish")})
         bij.append({"type": "roll", "shift": 1})
-    bij.append({"type": "nsc", "knots": K, "layers": layers})
+    bij.append({"type": "nsc", "knots": K, "layers": layers, "act": cfg.get("act", "swish")})
     return {"type": "chain", "bijectors": bij}
 
 
@@ -123,7 +133,7 @@ def build_flow(cfg):
         if b["type"] == "shift_bounds":
             mods.append(bi.ShiftBounds(margin=b["margin"], bounds=b["bounds"]))
         elif b["type"] == "nsc":
-            mods.append(bi.NeuralSplineCoupling(knots=b["knots"], layers=tuple(b["layers"])))
+            mods.append(bi.NeuralSplineCoupling(knots=b["knots"], layers=tuple(b["layers"]), act=b.get("act", "swish")))
         else:
             mods.append(bi.Roll(b["shift"]))
     return zf.Flow(bi.Chain(mods), latent=latent)

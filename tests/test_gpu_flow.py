@@ -72,10 +72,11 @@ def check_lp(lp, case, tag=""):
 
 
 WIDE_SHAPES = ["d6", "d8", "d16", "d7k32c2", "d4k32", "d3k32", "d4h256k8", "d5h64"]
+from tests.flowcases import ACTS  # noqa: E402  (NeuralSplineCoupling.act other than swish: fp32 kernel)
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"]
-                         + WIDE_SHAPES)
+                         + WIDE_SHAPES + ACTS)
 @pytest.mark.parametrize("N", [1, 1000, 4096])
 def test_log_prob_parity(name, N):
     case = make_case(name, N=N, seed=11)
@@ -87,7 +88,8 @@ def test_log_prob_parity_cfg5():
     check_lp(gpu_log_prob(case), case, "cfg5")
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES)
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
+                         + ["relu", "gelu", "sigmoid"])
 def test_inverse_parity(name):
     case = make_case(name, N=2000, seed=13)
     rng = np.random.default_rng(7)
@@ -269,7 +271,7 @@ def test_golden_edges(name):
 X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
 
 
-@pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"])
+@pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"] + ACTS)
 def test_kernel_selection(name, monkeypatch):
     case = make_case(name, N=8, seed=30)
     _, bf = _bound(case)

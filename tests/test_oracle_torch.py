@@ -18,14 +18,15 @@ def _np_loss(case, variables):
     return -lp.mean()
 
 
-@pytest.mark.parametrize("name", ["small", "cfg2", "cfg4", "odd"])
+@pytest.mark.parametrize("name", ["small", "cfg2", "cfg4", "odd", "relu", "gelu", "tanh", "softplus", "sigmoid", "elu",
+                                  "leaky_relu"])
 def test_torch_loss_equals_numpy_oracle(name):
     case = make_case(name, N=256, seed=71)
     loss, _ = OT.train_loss_and_grad(case["model"], case["variables"], case["x"], case["c"])
     assert loss == pytest.approx(_np_loss(case, case["variables"]), rel=1e-12, abs=1e-12)
 
 
-@pytest.mark.parametrize("name", ["small", "cfg4"])
+@pytest.mark.parametrize("name", ["small", "cfg4", "gelu", "elu"])
 def test_torch_grad_matches_central_differences(name):
     case = make_case(name, N=64, seed=72)
     _, g = OT.train_loss_and_grad(case["model"], case["variables"], case["x"], case["c"])
@@ -39,7 +40,7 @@ def test_torch_grad_matches_central_differences(name):
                 for flat in rng.choice(arr.size, size=min(3, arr.size), replace=False):
                     i = np.unravel_index(flat, arr.shape)
                     old = arr[i]
-                    h = 1e-3 * max(1e-2, abs(float(old)))
+                    h = 1e-5 * max(1e-2, abs(float(old)))  # small: elu and relu are only C1 / C0
                     vals = []
                     for s in (+1, -1):
                         arr[i] = np.float32(old + s * h)

@@ -7,7 +7,7 @@ Public surface mirrors the reference package (src/zenflow/__init__.py):
 in include/zenflow_amd.h."""
 
 from .flow import BoundFlow, Flow
-from . import bijectors, distributions, io, utils
+from . import activations, bijectors, distributions, io, utils
 from .io import load_variables, save_variables
 from .random import PRNGKey
 from .train import Optimizer, adamw, nadamw, train

@@ -28,6 +28,13 @@ ZF_LATENT_BETA = 2
 ZF_LATENT_TRUNCNORM = 3
 ZF_LATENT_UNIFORM = 4
 ZF_ACT_SWISH = 0
+ZF_ACT_RELU = 1
+ZF_ACT_TANH = 2
+ZF_ACT_SIGMOID = 3
+ZF_ACT_GELU = 4
+ZF_ACT_SOFTPLUS = 5
+ZF_ACT_ELU = 6
+ZF_ACT_LEAKY_RELU = 7
 ZF_SB_NONE = 0
 ZF_SB_BOTH = 1
 ZF_SB_LOWER = 2

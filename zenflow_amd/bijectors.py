@@ -27,9 +27,7 @@ __all__ = [
 ]
 
 
-def swish(x):
-    """Marker for flax.linen.swish (the only activation the kernels implement)."""
-    raise RuntimeError("zenflow_amd.bijectors.swish is evaluated inside the HIP kernel")
+from .activations import act_code, act_name, swish  # noqa: E402  (flax.linen.swish, the reference default)
 
 
 def _c_dims(c) -> int:
@@ -219,15 +217,16 @@ class NeuralSplineCoupling(Bijector):
     """Rational-quadratic spline coupling (bijectors.py:300-371).
 
     The upper half ``xc = x[:, D//2:]`` (plus conditions ``c``) drives a
-    conditioner MLP ``BatchNorm -> [Dense(w), swish]* -> Dense(dt*(3K-1))``
+    conditioner MLP ``BatchNorm -> [Dense(w), act]* -> Dense(dt*(3K-1))``
     whose outputs parametrise a monotone RQ spline on ``xt = x[:, :D//2]``.
-    The MLP runs on fp32 MFMA with activations resident in registers; the
-    spline + log-det run in the same kernel's epilogue."""
+    The MLP runs on MFMA with activations resident in registers; the
+    spline + log-det run in the same kernel's epilogue.  ``act``: swish (the
+    reference default) or another activation of ``zenflow_amd.activations``
+    (by function, name, or a callable of that name such as ``nn.relu``)."""
 
     def __init__(self, knots: int = 16, layers: Sequence[int] = (128, 128),
                  act: Callable = swish):
-        if act is not swish and getattr(act, "__name__", "") not in ("swish", "silu"):
-            raise NotImplementedError("only the swish activation is implemented")
+        self.act_code = act_code(act)  # NotImplementedError for an activation the kernels lack
         self.knots = int(knots)
         self.layers = tuple(int(w) for w in layers)
         self.act = act
@@ -263,7 +262,8 @@ class NeuralSplineCoupling(Bijector):
             fan_in = w
 
     def __repr__(self):
-        return f"NeuralSplineCoupling(knots={self.knots}, layers={self.layers})"
+        a = "" if self.act_code == L.ZF_ACT_SWISH else f", act={act_name(self.act_code)}"
+        return f"NeuralSplineCoupling(knots={self.knots}, layers={self.layers}{a})"
 
 
 def rolling_spline_coupling(

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
         for (int r4 = 0; r4 < 4; ++r4) wc[r4] = f[r4 * 64];
       }
       floatx16 hb[T];
-      layer0<T>(op, blob, xs, cin, row, valid, C, rot, D, s, hh, lane, hb);
+      layer0<T>(op, blob, xs, cin, row, valid, C, rot, D, s, hh, lane, hb, T, op.act);
       // Hidden layers 1..n_hidden-1 (:343-345): HP x HP on MFMA.  The last
       // tile of each layer prefetches the next layer's first chunk.
       for (int l = 1; l < op.n_hidden; ++l) {
@@ -207,8 +207,13 @@ __global__ __launch_bounds__(kWaves * 64, (HP <= 128 ? 2 : 1)) void flow_kernel(
           floatx4 bv[4];
           bias_tile(blob + op.b[l] + o * 32, hh, bv);
           floatx16 acc = mfma_tile<T>(wl + o * T * 256, nx, wc, hb);
+          if (op.act == ZF_ACT_SWISH) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[r] = swish(acc[r] + bv[r >> 2][r & 3]);
+            for (int r = 0; r < 16; ++r) acc[r] = swish(acc[r] + bv[r >> 2][r & 3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = act_other(op.act, acc[r] + bv[r >> 2][r & 3]);
+          }
           ho[o] = acc;
         }
 #pragma unroll
@@ -359,7 +364,7 @@ int validate(const zf_flow_desc* desc) {
       if (op.n_hidden < 1 || op.n_hidden > 16) return enotsup("n_hidden must be in [1, 16]");
       for (int l = 0; l < op.n_hidden; ++l)
         if (op.hidden[l] < 1 || op.hidden[l] > 256) return enotsup("hidden width must be in [1, 256]");
-      if (op.act != ZF_ACT_SWISH) return enotsup("only the swish activation is implemented");
+      if (op.act < 0 || op.act >= ZF_ACT_COUNT) return einval("op %d: unknown activation %d", i, op.act);
     } else if (op.kind != ZF_OP_ROLL && op.kind != ZF_OP_SHIFT_BOUNDS) {
       return einval("op %d: unknown kind %d", i, op.kind);
     }

@@ -4,6 +4,7 @@
 // op steps that do not touch the conditioner GEMMs (ShiftBounds, the
 // BatchNorm + first Dense layer, the latent log_prob epilogue).
 #pragma once
+#include "zf_act.h"
 #include "zf_internal.h"
 #include "zf_random.h"
 #include "zf_spline.h"
@@ -217,7 +218,7 @@ template <int T>
 __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict__ blob, const float* xs,
                                        const float* __restrict__ cin, long long row, bool valid, int C,
                                        int rot, int D, int s, int hh, int lane, floatx16 (&hb)[T],
-                                       int swish_tiles = T) {
+                                       int swish_tiles = T, int act = ZF_ACT_SWISH) {
   const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
   const int DCp = 2 * KS0;
   const float* bn = blob + op.bn;
@@ -236,6 +237,13 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
   }
   // swish of tiles [0, swish_tiles): the bf16x3 kernel defers the others into
   // the next layer's MFMA stream
+  if (act != ZF_ACT_SWISH) {  // the fp32 kernel's other activations (act is wave-uniform)
+#pragma unroll
+    for (int o = 0; o < T; ++o)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hb[o][r] = act_other(act, hb[o][r]);
+    return;
+  }
 #pragma unroll
   for (int o = 0; o < T; ++o)
     if (o < swish_tiles)

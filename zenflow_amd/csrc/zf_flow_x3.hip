@@ -44,6 +44,7 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind != ZF_OP_NSC) continue;
+    if (op.act != ZF_ACT_SWISH) return false;  // the split kernel fuses swish only
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }

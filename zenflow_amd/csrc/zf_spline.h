@@ -172,16 +172,21 @@ __device__ __forceinline__ RqsBin rqs_bin_regs_sl(float v, const float (&w)[K], 
 template <bool FWD, int K, class TF>
 __device__ __forceinline__ RqsBin rqs_bin_monotone(float v, const float (&w)[K], const float (&h)[K],
                                                    const float (&sl)[K - 1], const TF& sp) {
-  float xk = 0.f, yk = 0.f, sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  // knot 0 (at 0) latched up front: for v >= 0 it is the first knot <= v,
+  // and for v < 0 (out of bounds: identity) or NaN the bin is unused
+  float sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
   float lo = 0.f, hi = (K > 1) ? sl[0] : 0.f;  // logits of dk, dk+1 at the current bin
+  float xk = w[0], yk = h[0];
+  // branch-free latch (selects, not exec-masked moves)
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const float kk = FWD ? xk : yk;
-    if (kk <= v) {
-      sxk = xk; syk = yk; sw = w[j]; sh = h[j];
-      lo = (j >= 1) ? sl[j - 1] : 0.f;
-      hi = (j + 1 < K) ? sl[j] : 0.f;
-    }
+  for (int j = 1; j < K; ++j) {
+    const bool c = (FWD ? xk : yk) <= v;
+    sxk = c ? xk : sxk;
+    syk = c ? yk : syk;
+    sw = c ? w[j] : sw;
+    sh = c ? h[j] : sh;
+    lo = c ? sl[j - 1] : lo;
+    hi = c ? ((j + 1 < K) ? sl[j] : 0.f) : hi;
     xk = xk + w[j];
     yk = yk + h[j];
   }

@@ -9,6 +9,7 @@
 // kernel; everything else is per-row elementwise / per-column reductions.
 // All parameters and gradients live in the natural FLAX blob layout of
 // zf_flow_plan on the device.
+#include "zf_act.h"
 #include "zf_internal.h"
 #include "zf_spline.h"
 
@@ -41,8 +42,9 @@ __host__ __device__ __forceinline__ int pmodi(int a, int m) {
 // loads are in flight in registers while the current one is multiplied.
 // Epilogues fused into the store:
 //   kEpiNone   C = acc
-//   kEpiBias   z = acc + bias[n]; C = z; H = swish(z) if H (flax.linen.swish)
-//   kEpiDSwish C = acc * swish'(Z[m, n])  (gradient through the activation)
+//   kEpiBias   z = acc + bias[n]; C = z; H = act(z) if H (flax.linen.swish, or
+//              the op's other activation, zf_act.h)
+//   kEpiDSwish C = acc * act'(Z[m, n])  (gradient through the activation)
 // WG (weight gradients, split-K over the batch): block z multiplies rows
 // [z*KC, (z+1)*KC) into part[z][M+1][N]; row M is the bias gradient, the
 // column sums of the B tile (op(B) = layer-output gradient), which blocks with
@@ -56,7 +58,8 @@ template <int BM, int BN, bool TA, bool TB, bool WG>
 __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                     int ldc, int epi, const float* __restrict__ bias,
-                                                    float* __restrict__ H, const float* __restrict__ Z, int KC) {
+                                                    float* __restrict__ H, const float* __restrict__ Z, int KC,
+                                                    int act) {
   constexpr int NA = BM * MBK / 256, NB = BN * MBK / 256;  // tile elements per thread
   constexpr int TM = BM / 64, TN = BN / 64;                // 32x32 tiles per wave
   __shared__ float As[MBK][BM + 1];
@@ -182,10 +185,15 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
           float v = acc[0][i][j][q];
           if (epi == kEpiBias) {
             v = v + bias[n];
-            if (H) H[o] = v * sigmoidf(v);
+            if (H) H[o] = act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
           } else if (epi == kEpiDSwish) {
-            const float z = Z[o], sg = sigmoidf(z);
-            v = v * (sg + z * sg * (1.0f - sg));
+            const float z = Z[o];
+            if (act == ZF_ACT_SWISH) {
+              const float sg = sigmoidf(z);
+              v = v * (sg + z * sg * (1.0f - sg));
+            } else {
+              v = v * act_other_grad(act, z);
+            }
           }
           C[o] = v;
         }
@@ -194,25 +202,25 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
 
 template <int T>
 void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
-                 hipStream_t st, int epi, const float* bias, float* H, const float* Z) {
+                 hipStream_t st, int epi, const float* bias, float* H, const float* Z, int act) {
   const dim3 grid((N + T - 1) / T, (M + T - 1) / T);
   if (!tb)
     hipLaunchKernelGGL((mgemm_kernel<T, T, false, false, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, bias, H, Z, 0);
+                       ldc, epi, bias, H, Z, 0, act);
   else
     hipLaunchKernelGGL((mgemm_kernel<T, T, false, true, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, bias, H, Z, 0);
+                       ldc, epi, bias, H, Z, 0, act);
 }
 
 // C = A . op(B) with A row-major [M][K]; 128 x 128 tiles when they give at
 // least 512 blocks, 64 x 64 otherwise.
 int gemm(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
          hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
-         const float* Z = nullptr) {
+         const float* Z = nullptr, int act = ZF_ACT_SWISH) {
   if (M <= 0 || N <= 0) return ZF_OK;
   const long long big = (long long)((N + 127) / 128) * ((M + 127) / 128);
-  if (big >= 512) gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z);
-  else gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z);
+  if (big >= 512) gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
+  else gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
   ZF_CHECK_LAUNCH("mgemm_kernel");
   return ZF_OK;
 }
@@ -305,7 +313,8 @@ int wgrad(int M, int N, int B, const Leaves& lv, const float* A, const float* G,
   constexpr int T = 64;
   if ((int64_t)lv.n * (M + 1) * N > kWsFloats) return enotsup("training: weight-gradient workspace");
   hipLaunchKernelGGL((mgemm_kernel<T, T, true, false, true>), dim3((N + T - 1) / T, (M + T - 1) / T, lv.n),
-                     dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows);
+                     dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows,
+                     (int)ZF_ACT_SWISH);
   ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
   hipLaunchKernelGGL(wgrad_tree, dim3(blocks_for((int64_t)(M + 1) * N)), dim3(256), 0, st, M, N, lv.n, ws, dW, db);
   ZF_CHECK_LAUNCH("wgrad_tree");
@@ -1241,7 +1250,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         const int out_w = last ? dt * S : op.hidden[l];
         float* Z = last ? nb.P : nb.Z[l];
         rc = zf::gemm(false, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
-                      nat + op.off_b[l], last ? nullptr : nb.H[l]);
+                      nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act);
         if (rc) return rc;
         if (!last) {
           in = nb.H[l];
@@ -1311,7 +1320,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       float* gin = l == 0 ? nb.gU : gbufs[which];
       // (through swish of layer l-1 when l > 0)
       rc = zf::gemm(true, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
-                    l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr);
+                    l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act);
       if (rc) return rc;
       if (l > 0) {
         gout = gin;

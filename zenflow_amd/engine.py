@@ -119,7 +119,7 @@ class Program:
                 d.n_hidden = len(m.layers)
                 for l, w in enumerate(m.layers):
                     d.hidden[l] = int(w)
-                d.act = L.ZF_ACT_SWISH
+                d.act = int(m.act_code)
         n = ct.c_int64()
         lib = L.load_library()
         check(lib.zf_flow_plan(ct.byref(desc), ct.byref(n)), "zf_flow_plan")
