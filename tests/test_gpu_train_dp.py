@@ -8,7 +8,9 @@ ranks on one device), each on its half of every batch.  The trainer's batch
 reductions are fixed leaf trees whose shape depends on the global batch only,
 so both ranks must end with the bits ONE device gets on the whole batch:
 the same loss, the same gradient, and after three optimiser steps the same
-parameters and statistics — compared with ``array_equal``, not a tolerance."""
+parameters and statistics — compared with ``array_equal``, not a tolerance.
+65536 rows is past the batch at which the forward GEMMs switch to 128-row
+tiles (chosen by the global batch, so a 32768-row shard switches too)."""
 
 import os
 from pathlib import Path
@@ -23,7 +25,7 @@ WORKER = str(Path(__file__).resolve().parent / "dist_worker.py")
 
 
 @pytest.mark.parametrize("name,N,seed", [("cfg2", 1024, 81), ("cfg4", 2048, 82), ("d8", 1024, 83),
-                                         ("cfg2", 16384, 84)])
+                                         ("cfg2", 16384, 84), ("cfg2", 65536, 85)])
 def test_two_ranks_match_one_device_bitwise(tmp_path, name, N, seed):
     from zenflow_amd import _lib as L
     from zenflow_amd.launch import spawn

@@ -103,7 +103,10 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
   // summed pairwise at the end: a 256-long fp32 fma chain becomes four
   // 64-long ones (the input-gradient and forward GEMMs run K up to 256;
   // the weight-gradient chunks are 32 rows).
-  constexpr int NACC = (WG || TM * TN > 1) ? 1 : 4;  // 128-wide tiles: registers for one set only
+#ifndef ZF_TRAIN_NACC
+#define ZF_TRAIN_NACC 4
+#endif
+  constexpr int NACC = (WG || TM * TN > 1) ? 1 : ZF_TRAIN_NACC;  // 128-wide tiles: registers for one set only
   floatx16 acc[NACC][TM][TN];
 #pragma unroll
   for (int q = 0; q < NACC; ++q)
@@ -213,12 +216,15 @@ void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const fl
 }
 
 // C = A . op(B) with A row-major [M][K]; 128 x 128 tiles when they give at
-// least 512 blocks, 64 x 64 otherwise.
-int gemm(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
-         hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
+// least 512 blocks over the GLOBAL batch's Mg rows, 64 x 64 otherwise.  The
+// two tiles accumulate differently (one chain vs four interleaved), so the
+// choice follows the global batch: every data-parallel shard then runs the
+// kernel, and gets the bits, of the one-device step.
+int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
+         int ldc, hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
          const float* Z = nullptr, int act = ZF_ACT_SWISH) {
   if (M <= 0 || N <= 0) return ZF_OK;
-  const long long big = (long long)((N + 127) / 128) * ((M + 127) / 128);
+  const long long big = (long long)((N + 127) / 128) * ((Mg + 127) / 128);
   if (big >= 512) gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
   else gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
   ZF_CHECK_LAUNCH("mgemm_kernel");
@@ -228,7 +234,7 @@ int gemm(bool tb, int M, int N, int K, const float* A, int lda, const float* B, 
 inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
 // Split-K workspace (floats) shared by the batch reductions below.
-constexpr int64_t kWsFloats = 8ll << 20;
+constexpr int64_t kWsFloats = 32ll << 20;
 
 // ---- batch reductions: row leaves + one fixed pairwise tree ----------------
 // Every sum over the batch rows (weight and bias gradients, BatchNorm sums
@@ -242,7 +248,8 @@ constexpr int64_t kWsFloats = 8ll << 20;
 // the same tree.  So every rank gets the same bits, and R ranks reproduce
 // one rank's bits on the same global batch (R a power of two dividing the
 // leaf count, shards of B/R rows, B a multiple of the leaf count).
-constexpr int kMaxLeaves = 64;
+constexpr int kMaxLeaves = 64;        // one tree level (registers)
+constexpr int kLeafCap = kMaxLeaves * kMaxLeaves;  // two levels: up to 4096 leaves
 
 inline int pow2floor(long long v) {
   int p = 1;
@@ -264,43 +271,93 @@ inline Leaves leaves_for(long long B_loc, long long Bg, int world, int cap) {
   return l;
 }
 
-// Pairwise tree over p[0], p[stride], ..., p[(n-1) stride] (n <= 64) in fp64:
-// level s adds element i + s into i for i a multiple of 2s (the perfect tree
-// for a power of two; a shorter tail just joins later).
-template <typename TI>
+// Pairwise tree over p[0], p[stride], ..., p[(n-1) stride] (n <= NMAX <= 64)
+// in fp64: level s adds element i + s into i for i a multiple of 2s (the
+// perfect tree for a power of two; a shorter tail just joins later).  NMAX
+// only sizes the register array: every NMAX >= n gives the same bits.
+template <int NMAX, typename TI>
 __device__ __forceinline__ double tree_n(const TI* __restrict__ p, long long stride, int n) {
-  double v[kMaxLeaves];
+  double v[NMAX];
 #pragma unroll
-  for (int i = 0; i < kMaxLeaves; ++i) v[i] = i < n ? (double)p[i * stride] : 0.0;
+  for (int i = 0; i < NMAX; ++i) v[i] = i < n ? (double)p[i * stride] : 0.0;
 #pragma unroll
-  for (int s = 1; s < kMaxLeaves; s *= 2)
+  for (int s = 1; s < NMAX; s *= 2)
 #pragma unroll
-    for (int i = 0; i < kMaxLeaves; i += 2 * s)
+    for (int i = 0; i < NMAX; i += 2 * s)
       if (i + s < n) v[i] = v[i] + v[i + s];
   return v[0];
 }
 
+// The same tree in place over LDS columns (leaf i of column k at
+// p[i * stride + k]), all threads of the block taking part, one barrier per
+// level: the same pairings and operand order as tree_n.  Result in p[k].
+__device__ __forceinline__ void lds_tree(double* p, int n, int ncols, int stride) {
+  for (int s = 1; s < n; s *= 2) {
+    const int pairs = (n + 2 * s - 1) / (2 * s);
+    for (int t = threadIdx.x; t < pairs * ncols; t += blockDim.x) {
+      const int j = t / ncols, k = t - j * ncols, i = 2 * s * j;
+      if (i + s < n) p[i * stride + k] = p[i * stride + k] + p[(i + s) * stride + k];
+    }
+    __syncthreads();
+  }
+}
+
+// Launch KERNEL<..., NMAX> with the smallest register tree that holds n leaves.
+#define ZF_NMAX_DISPATCH(n, LAUNCH) \
+  do {                              \
+    if ((n) <= 8) LAUNCH(8);        \
+    else if ((n) <= 16) LAUNCH(16); \
+    else if ((n) <= 32) LAUNCH(32); \
+    else LAUNCH(64);                \
+  } while (0)
+
 // out[k] = tree over n leaves of part[leaf * N + k]
-template <typename TI>
+template <typename TI, int NMAX>
 __global__ void tree_cols_kernel(const TI* __restrict__ part, int n, long long N, double* __restrict__ out) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < N) out[k] = tree_n(part + k, N, n);
+  if (k < N) out[k] = tree_n<NMAX>(part + k, N, n);
+}
+
+// First level of a two-level tree: out[g * N + k] = tree over the 64 leaves
+// [64 g, 64 g + 64) of part (a perfect subtree of the power-of-two leaf tree,
+// so the second level over the group roots completes the same tree).
+template <typename TI>
+__global__ void tree_groups_kernel(const TI* __restrict__ part, int groups, long long N, double* __restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)groups * N) return;
+  const long long g = t / N, k = t - g * N;
+  out[t] = tree_n<kMaxLeaves>(part + g * kMaxLeaves * N + k, N, kMaxLeaves);
 }
 
 // same, then the final fp32 rounding (the gradient handed to the optimiser)
+template <int NMAX>
 __global__ void tree_cols_cast_kernel(const double* __restrict__ part, int n, long long N, float* __restrict__ out) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < N) out[k] = (float)tree_n(part + k, N, n);
+  if (k < N) out[k] = (float)tree_n<NMAX>(part + k, N, n);
 }
 
-// dW/db from the split-K partials part[leaf][M+1][N] (fp32 leaf GEMMs),
-// combined by the leaf tree into the fp64 gradient accumulator.
-__global__ void wgrad_tree(int M, int N, int n, const float* __restrict__ part, double* __restrict__ dW,
-                           double* __restrict__ db) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+// dW/db from the split-K partials part[leaf][M+1][N] (fp32 leaf GEMMs, or
+// their fp64 group roots), combined by the leaf tree into the fp64 gradient
+// accumulator.
+// dW / db from the n (a power of two) leaf partials of each element: the
+// four waves of a block each reduce a perfect subtree of n / 4 consecutive
+// leaves for 64 elements (n < 4: one wave per leaf), joined as the top two
+// levels of the same tree — four times the waves of a thread-per-element tree
+// for the same bits.
+template <typename TI, int NMAX>
+__global__ __launch_bounds__(256) void wgrad_tree(int M, int N, int n, const TI* __restrict__ part,
+                                                  double* __restrict__ dW, double* __restrict__ db) {
+  __shared__ double r[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int P = n < 4 ? n : 4, m = n / P;
+  const long long idx = (long long)blockIdx.x * 64 + lane;
   const long long MN1 = (long long)(M + 1) * N;
-  if (idx >= MN1) return;
-  const double v = tree_n(part + idx, MN1, n);
+  if (w < P && idx < MN1) r[w][lane] = tree_n<NMAX>(part + (long long)w * m * MN1 + idx, MN1, m);
+  __syncthreads();
+  if (w != 0 || idx >= MN1) return;
+  double v = r[0][lane];
+  if (P == 2) v = v + r[1][lane];
+  else if (P == 4) v = (v + r[1][lane]) + (r[2][lane] + r[3][lane]);
   if (idx < (long long)M * N) dW[idx] = v;
   else db[idx - (long long)M * N] = v;
 }
@@ -309,14 +366,27 @@ __global__ void wgrad_tree(int M, int N, int n, const float* __restrict__ part, 
 // G row-major [B][N] (gradient of the layer output): one split-K block per
 // leaf (rows [z lv.rows, (z+1) lv.rows)), then wgrad_tree.
 int wgrad(int M, int N, int B, const Leaves& lv, const float* A, const float* G, double* dW, double* db, float* ws,
-          hipStream_t st) {
+          double* ws2, hipStream_t st) {
   constexpr int T = 64;
-  if ((int64_t)lv.n * (M + 1) * N > kWsFloats) return enotsup("training: weight-gradient workspace");
+  const int64_t MN1 = (int64_t)(M + 1) * N;
+  if ((int64_t)lv.n * MN1 > kWsFloats) return enotsup("training: weight-gradient workspace");
   hipLaunchKernelGGL((mgemm_kernel<T, T, true, false, true>), dim3((N + T - 1) / T, (M + T - 1) / T, lv.n),
                      dim3(256), 0, st, M, N, B, A, M, G, N, ws, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows,
                      (int)ZF_ACT_SWISH);
   ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
-  hipLaunchKernelGGL(wgrad_tree, dim3(blocks_for((int64_t)(M + 1) * N)), dim3(256), 0, st, M, N, lv.n, ws, dW, db);
+  if (lv.n <= kMaxLeaves) {
+#define ZF_L(NM) hipLaunchKernelGGL((wgrad_tree<float, NM>), dim3(blocks_for(MN1, 64)), dim3(256), 0, st, M, N, lv.n, ws, dW, db)
+    ZF_NMAX_DISPATCH(lv.n < 4 ? 1 : lv.n / 4, ZF_L);
+#undef ZF_L
+  } else {  // two levels: groups of 64 leaves, then their roots
+    const int groups = lv.n / kMaxLeaves;
+    hipLaunchKernelGGL(tree_groups_kernel<float>, dim3(blocks_for((int64_t)groups * MN1)), dim3(256), 0, st, ws,
+                       groups, MN1, ws2);
+    ZF_CHECK_LAUNCH("tree_groups_kernel");
+#define ZF_L(NM) hipLaunchKernelGGL((wgrad_tree<double, NM>), dim3(blocks_for(MN1, 64)), dim3(256), 0, st, M, N, groups, ws2, dW, db)
+    ZF_NMAX_DISPATCH(groups < 4 ? 1 : groups / 4, ZF_L);
+#undef ZF_L
+  }
   ZF_CHECK_LAUNCH("wgrad_tree");
   return ZF_OK;
 }
@@ -358,8 +428,22 @@ __global__ void leaf_sum_kernel(const double* __restrict__ x, int B, int rows, i
   p[z] = a;
 }
 
-inline int launch_tree_cols(const double* part, int n, long long N, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(tree_cols_kernel<double>, dim3(blocks_for(N)), dim3(256), 0, st, part, n, N, out);
+// out[k] = tree over n leaves (a power of two up to kLeafCap, or any n <= 64)
+// of part[leaf * N + k]; tmp: (n / 64) * N doubles for the two-level case.
+inline int launch_tree_cols(const double* part, int n, long long N, double* out, hipStream_t st,
+                            double* tmp = nullptr) {
+  if (n > kMaxLeaves) {
+    if (!tmp) return einval("tree over %d leaves needs a workspace", n);
+    const int groups = n / kMaxLeaves;
+    hipLaunchKernelGGL(tree_groups_kernel<double>, dim3(blocks_for((long long)groups * N)), dim3(256), 0, st, part,
+                       groups, N, tmp);
+    ZF_CHECK_LAUNCH("tree_groups_kernel");
+    part = tmp;
+    n = groups;
+  }
+#define ZF_L(NM) hipLaunchKernelGGL((tree_cols_kernel<double, NM>), dim3(blocks_for(N)), dim3(256), 0, st, part, n, N, out)
+  ZF_NMAX_DISPATCH(n, ZF_L);
+#undef ZF_L
   ZF_CHECK_LAUNCH("tree_cols_kernel");
   return ZF_OK;
 }
@@ -732,7 +816,7 @@ __global__ void bn_bwd_kernel(const float* __restrict__ gUbn, const float* __res
 // leaf_colsums + tree + bn_bwd + scatter reverse): the same leaf_sums2 per
 // (leaf, column) and the same tree_n over the leaves, here through LDS.
 constexpr long long kBnSmall = 1ll << 14;
-constexpr int kBnLeafCap = kMaxLeaves;  // leaves of a BatchNorm sum (both paths)
+constexpr int kBnLeafCap = kLeafCap;  // leaves of a BatchNorm sum (both paths)
 
 __global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s, const float* __restrict__ c,
                                                      float* __restrict__ Uhat, float* __restrict__ Ubn,
@@ -749,9 +833,11 @@ __global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s
     leaf_sums2([&](int b) { return u_at(b, k); }, [&](int b) { return u_at(b, k); }, b0, b1, p1[t], p2[t]);
   }
   __syncthreads();
+  lds_tree(p1, n, DC, DC);
+  lds_tree(p2, n, DC, DC);
   if (tid < DC) {
     float mean, rstd;
-    bn_stats_one(tree_n(p1 + tid, DC, n), tree_n(p2 + tid, DC, n), B, tid, DC, nat_bn, mean, rstd, update);
+    bn_stats_one(p1[tid], p2[tid], B, tid, DC, nat_bn, mean, rstd, update);
     smean[tid] = mean;
     srstd[tid] = rstd;
     mean_out[tid] = mean;
@@ -786,8 +872,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_small(const float* __restrict__ g
                b0, b1, p1[t], p2[t]);
   }
   __syncthreads();
+  lds_tree(p1, n, DC, DC);
+  lds_tree(p2, n, DC, DC);
   if (tid < DC) {
-    const double sg = tree_n(p1 + tid, DC, n), sgu = tree_n(p2 + tid, DC, n);
+    const double sg = p1[tid], sgu = p2[tid];
     g_scale[tid] = sgu;
     g_bias[tid] = sg;
     mg_s[tid] = bn_mean_term(scale[tid], sg, B);
@@ -953,7 +1041,9 @@ struct zf_trainer {
   float* d_g0 = nullptr;      // [bmax][D]
   float* d_g1 = nullptr;
   float* d_small = nullptr;   // per-column scratch (ShiftBounds min / max)
-  double* d_leaf = nullptr;   // leaf partials of the BatchNorm sums / loss [kMaxLeaves][128]
+  double* d_leaf = nullptr;   // leaf partials of the BatchNorm sums / loss [kLeafCap][128]
+  double* d_leaf2 = nullptr;  // first-level tree roots [kLeafCap / 64][128]
+  double* d_ws2 = nullptr;    // first-level roots of the split-K partials
   double* d_roots = nullptr;  // [0,128): tree roots of one reduction; [128]: the loss
   double* d_rowloss = nullptr;  // [bmax] per-row loss terms
   double* d_g64 = nullptr;    // fp64 gradient accumulator (blob layout)
@@ -1047,7 +1137,9 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_g0 = zf::dmalloc(t, B * D, rc);
   t->d_g1 = zf::dmalloc(t, B * D, rc);
   t->d_small = zf::dmalloc(t, 8 * 256, rc);
-  t->d_leaf = (double*)zf::dmalloc(t, 2 * zf::kMaxLeaves * 128, rc);
+  t->d_leaf = (double*)zf::dmalloc(t, 2 * zf::kLeafCap * 128, rc);
+  t->d_leaf2 = (double*)zf::dmalloc(t, 2 * (zf::kLeafCap / zf::kMaxLeaves) * 128, rc);
+  t->d_ws2 = (double*)zf::dmalloc(t, 2 * (zf::kWsFloats / zf::kMaxLeaves), rc);
   t->d_roots = (double*)zf::dmalloc(t, 2 * 256, rc);
   t->d_rowloss = (double*)zf::dmalloc(t, 2 * B, rc);
   t->d_g64 = (double*)zf::dmalloc(t, 2 * need, rc);
@@ -1234,7 +1326,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         hipLaunchKernelGGL(leaf_colsums_kernel, dim3(blocks_for((int64_t)lbn.n * DC)), dim3(256), 0, st, nb.U,
                            nullptr, B, DC, lbn.rows, lbn.n, t->d_leaf);
         ZF_CHECK_LAUNCH("leaf_colsums_kernel");
-        if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st))) return rc;
+        if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st, t->d_leaf2))) return rc;
         if ((rc = dp_combine(t, t->d_roots, 2 * DC, st))) return rc;
         hipLaunchKernelGGL(zf::bn_stats_kernel, dim3(1), dim3(64), 0, st, t->d_roots, t->d_roots + DC, Bg, DC, bn,
                            nb.mean, nb.rstd, update_stats);
@@ -1249,7 +1341,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         const bool last = (l == op.n_hidden);
         const int out_w = last ? dt * S : op.hidden[l];
         float* Z = last ? nb.P : nb.Z[l];
-        rc = zf::gemm(false, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
+        rc = zf::gemm(false, Bg, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
                       nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act);
         if (rc) return rc;
         if (!last) {
@@ -1280,10 +1372,11 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
                      B, Bg, D, rot, lt, a, betac, tnm, g, t->d_rowloss);
   ZF_CHECK_LAUNCH("latent_loss_kernel");
   {
-    const Leaves ll = leaves_for(B, Bg, W, kMaxLeaves);
-    hipLaunchKernelGGL(leaf_sum_kernel, dim3(1), dim3(64), 0, st, t->d_rowloss, B, ll.rows, ll.n, t->d_leaf);
+    const Leaves ll = leaves_for(B, Bg, W, kLeafCap);
+    hipLaunchKernelGGL(leaf_sum_kernel, dim3(blocks_for(ll.n, 64)), dim3(64), 0, st, t->d_rowloss, B, ll.rows, ll.n,
+                       t->d_leaf);
     ZF_CHECK_LAUNCH("leaf_sum_kernel");
-    if ((rc = launch_tree_cols(t->d_leaf, ll.n, 1, loss_slot(t), st))) return rc;
+    if ((rc = launch_tree_cols(t->d_leaf, ll.n, 1, loss_slot(t), st, t->d_leaf2))) return rc;
     if ((rc = dp_combine(t, loss_slot(t), 1, st))) return rc;
   }
   // ---- reverse ----
@@ -1312,14 +1405,14 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       const float* hin = l == 0 ? nb.Ubn : nb.H[l - 1];
       // dW_l = hin^T . gout ; db_l = colsum(gout): leaves capped by the
       // split-K workspace (a power of two, the same on every rank)
-      const int cap = pow2floor(std::min<int64_t>(kMaxLeaves, std::max<int64_t>(1, kWsFloats / ((int64_t)(in_w + 1) * out_w))));
+      const int cap = pow2floor(std::min<int64_t>(kLeafCap, std::max<int64_t>(1, kWsFloats / ((int64_t)(in_w + 1) * out_w))));
       rc = zf::wgrad(in_w, out_w, B, leaves_for(B, Bg, W, cap), hin, gout, G64 + op.off_w[l], G64 + op.off_b[l],
-                     t->d_ws, st);
+                     t->d_ws, t->d_ws2, st);
       if (rc) return rc;
       // g_in = gout . W_l^T
       float* gin = l == 0 ? nb.gU : gbufs[which];
       // (through swish of layer l-1 when l > 0)
-      rc = zf::gemm(true, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
+      rc = zf::gemm(true, Bg, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
                     l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act);
       if (rc) return rc;
       if (l > 0) {
@@ -1341,7 +1434,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       hipLaunchKernelGGL(leaf_colsums_kernel, dim3(blocks_for((int64_t)lbn.n * DC)), dim3(256), 0, st, nb.gU,
                          nb.Uhat, B, DC, lbn.rows, lbn.n, t->d_leaf);
       ZF_CHECK_LAUNCH("leaf_colsums_kernel");
-      if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st))) return rc;
+      if ((rc = launch_tree_cols(t->d_leaf, lbn.n, 2 * DC, t->d_roots, st, t->d_leaf2))) return rc;
       ZF_TRY_HIP(hipMemcpyAsync(gbn + 3 * DC, t->d_roots, DC * sizeof(double), hipMemcpyDeviceToDevice, st));
       ZF_TRY_HIP(hipMemcpyAsync(gbn + 2 * DC, t->d_roots + DC, DC * sizeof(double), hipMemcpyDeviceToDevice, st));
       if ((rc = dp_combine(t, t->d_roots, 2 * DC, st))) return rc;
@@ -1361,8 +1454,10 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
   if (W > 1) {
     rc = t->comm.allgather(t->comm.ctx, G64, t->d_gath, (size_t)t->nat_floats * sizeof(double), st);
     if (rc) return rc;
-    hipLaunchKernelGGL(tree_cols_cast_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st,
-                       (const double*)t->d_gath, W, (long long)t->nat_floats, G);
+#define ZF_L(NM) hipLaunchKernelGGL((tree_cols_cast_kernel<NM>), dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, \
+                                    (const double*)t->d_gath, W, (long long)t->nat_floats, G)
+    ZF_NMAX_DISPATCH(W, ZF_L);
+#undef ZF_L
     ZF_CHECK_LAUNCH("tree_cols_cast_kernel");
   } else {
     hipLaunchKernelGGL(cast_f64_f32_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, G64,

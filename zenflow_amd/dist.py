@@ -115,7 +115,7 @@ class HostAllgather:
         pass
 
 
-def reduction_leaves(rows: int, global_rows: int, world: int, cap: int = 64) -> Tuple[int, int]:
+def reduction_leaves(rows: int, global_rows: int, world: int, cap: int = 4096) -> Tuple[int, int]:
     """(leaves on this rank, rows per leaf) of every batch reduction of the
     trainer — the host mirror of zf_train.hip ``leaves_for``: ~32 rows per
     leaf, at most ``cap`` (a power of two) leaves in the global batch, a
@@ -140,7 +140,7 @@ def tree_sum(leaves: np.ndarray) -> np.ndarray:
     return v[0]
 
 
-def leaf_tree_colsum(x: np.ndarray, global_rows: int, world: int, cap: int = 64) -> np.ndarray:
+def leaf_tree_colsum(x: np.ndarray, global_rows: int, world: int, cap: int = 4096) -> np.ndarray:
     """This rank's subtree root of the column sums of ``x`` (rows x cols,
     fp32): leaves of ``reduction_leaves`` rows summed in row order in fp64,
     then ``tree_sum`` — the schedule of the trainer's BatchNorm sums."""
