@@ -54,35 +54,12 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// flax.linen.swish = x * sigmoid(x) = x / (1 + exp(-x)) (bijectors.py:319).
-// 0: v * rcp(1 + 2^(-v*log2e))  (6 VALU, ~|v|*6e-8 relative error)
-// 1: compensated exp argument (exact residual of t = -x*log2e plus the log2e
-//    tail) + Newton reciprocal (~1 ulp, 16 VALU)
-// 2: expf + IEEE division (reference form)
-// All three give the same mean log_prob error as the fp32 oracle
-// (scripts/diag_parity.py); 0 is the default.
-#ifndef ZF_SWISH_MODE
-#define ZF_SWISH_MODE 0
-#endif
+// flax.linen.swish = x * sigmoid(x) = x / (1 + exp(-x)) (bijectors.py:319):
+// v * rcp(1 + 2^(-v*log2e)) (~|v|*6e-8 relative error; a compensated exp
+// argument with a Newton reciprocal, and expf with IEEE division, gave the
+// same mean log_prob error against the fp32 oracle, scripts/diag_parity.py).
 __device__ __forceinline__ float swish(float v) {
-#if ZF_SWISH_MODE == 0
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.44269504f));
-#elif ZF_SWISH_MODE == 2
-  return v * (1.0f / (1.0f + expf(-v)));
-#else
-  constexpr float kL2E = 1.44269502162933349609375f;  // fp32(log2 e)
-  constexpr float kL2ELo = 1.925963033500011e-08f;    // log2 e - kL2E
-  constexpr float kLn2 = 0.693147180559945f;
-  const float nv = -v;
-  const float t = nv * kL2E;
-  const float lo = __builtin_fmaf(nv, kL2E, -t) + nv * kL2ELo;
-  const float p = __builtin_amdgcn_exp2f(t);
-  const float e = (p == INFINITY) ? p : __builtin_fmaf(p, lo * kLn2, p);
-  const float d = 1.0f + e;
-  float r = __builtin_amdgcn_rcpf(d);
-  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
-  return v * r;
-#endif
 }
 
 // 1/x to ~0.5 ulp: hardware reciprocal + one Newton step.

@@ -76,18 +76,9 @@ struct XT<2> {
 
 // Hidden 256 (one wave per SIMD, nothing else to hide LDS latency or fill
 // MFMA issue gaps): A fragments one output tile ahead, and each group's
-// MFMAs interleaved with its VALU by sched_group_barrier (measured +4-5% at
-// cfg5; at T = 4 both were neutral to -12% and stay off).
-#ifndef ZF_X3_WIDE_SCHED
-#define ZF_X3_WIDE_SCHED 3
-#endif
-
-// f16x2, hidden <= 128: seed the accumulators with bias / us (1) instead of
-// joining the bias at the layer's end with one fma (0).
-#ifndef ZF_X3_SEED_SCALED
-#define ZF_X3_SEED_SCALED 1
-#endif
-
+// MFMAs interleaved with its VALU by sched_group_barrier, kWideSched VALU
+// per MFMA (measured +4-5% at cfg5; at T = 4 both were neutral to -12%).
+constexpr int kWideSched = 3;
 
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
@@ -113,16 +104,12 @@ __device__ __forceinline__ void split8(const floatx16& v, bf16x8& bh, bf16x8& bm
 }
 
 // Regs 8s..8s+7 of an (already scaled) activation tile -> hi / lo fp16x8
-// (RNE each; the residual x - hi is exact).  ZF_X3_MIXSPLIT: the lo term by
+// (RNE each; the residual x - hi is exact).  The lo term by
 // v_fma_mix{lo,hi}_f16 (x*1 - f32(hi) rounded to f16 in one instruction:
-// 3 instead of 5 VALU per value pair, bit-identical —
+// 3 instead of 5 VALU per value pair, bit-identical to sub + cvt —
 // tests/hip/f16_split_mix.hip).
-#ifndef ZF_X3_MIXSPLIT
-#define ZF_X3_MIXSPLIT 1
-#endif
 template <int S>
 __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& bl) {
-#if ZF_X3_MIXSPLIT
   // One asm statement for all eight lo terms, ending in `s_nop 1`: hipcc
   // pads no hazard inside or after an asm statement, and its outputs feed an
   // MFMA operand, which needs two wait states after a VALU write (without
@@ -149,17 +136,6 @@ __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& b
         "v"(v[8 * S + 5]), "v"(v[8 * S + 6]), "v"(v[8 * S + 7]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
   __builtin_memcpy(&bh, h, 16);
   __builtin_memcpy(&bl, l, 16);
-#else
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const floatx2 x = floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]};
-    const halfx2 h = __builtin_convertvector(x, halfx2);
-    const floatx2 r = x - __builtin_convertvector(h, floatx2);
-    const halfx2 l = __builtin_convertvector(r, halfx2);
-    bh[2 * i] = h[0]; bh[2 * i + 1] = h[1];
-    bl[2 * i] = l[0]; bl[2 * i + 1] = l[1];
-  }
-#endif
 }
 
 template <int NT, int S>
@@ -182,16 +158,11 @@ constexpr float kSwishPrescale = 1.44269504088896341f;
 // neither the exponent scale nor the activation scale costs an instruction.
 template <int NT>
 __device__ __forceinline__ float act_swish(float v, float c) {
-#if ZF_SWISH_MODE == 0
   if constexpr (NT == 2) {
     const float e = __builtin_amdgcn_exp2f(-v);
     return v * __builtin_amdgcn_rcpf(__builtin_fmaf(e, c, c));
   }
   return swish(v);
-#else
-  if constexpr (NT == 2) return swish(v * (1.0f / kSwishPrescale)) * (kSwishPrescale / c);
-  return swish(v);
-#endif
 }
 
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
@@ -416,7 +387,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
   }
-  if constexpr (T == 8 && ZF_X3_WIDE_SCHED > 0) {
+  if constexpr (T == 8) {
     // the k-step-0 split first, then every MFMA followed by its share of LDS
     // reads and VALU (split of k-step 1, the deferred swish)
     constexpr int kP = XT<NT>::kProd;
@@ -426,7 +397,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
     for (int i = 0; i < 2 * kP * NOUT; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if ((NT == 3 && i % 2 == 0) || (NT == 2 && i % 3 != 2)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x402, ZF_X3_WIDE_SCHED, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, kWideSched, 0);
     }
   }
   char* const t = p.cur;
@@ -441,9 +412,6 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 // (Q+1, 0) for the next group — so the bf16 split and the deferred swish sit
 // in the MFMA issue gaps of the same wave (cross-wave they would not overlap:
 // tests/hip/coexec_probe.hip modes 2 and 6).
-#ifndef ZF_X3_PIPE
-#define ZF_X3_PIPE 1
-#endif
 template <int NT, int T, int NOUT, int Q, bool HASB>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
@@ -513,46 +481,23 @@ __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p,
   }
 }
 
-// squareplus with a Newton-corrected reciprocal square root (one
-// transcendental instead of sqrt + rcp): ~0.5 ulp, like sqrtf.
-__device__ __forceinline__ float squareplus_rsq(float x) {
-  const float a = x * x + 4.0f;
-  const float r = __builtin_amdgcn_rsqf(a);
-  float sq = a * r;
-  sq = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * r, sq);
-  return 0.5f * (x + sq);
-}
-
-// Spline arithmetic of the split-MFMA kernel (ZF_X3_FASTSPLINE=1): the
-// spline parameters already differ from the reference's in the last ulp
+// Spline arithmetic of the split-MFMA kernel: the spline parameters already differ from the reference's in the last ulp
 // (GEMM summation order), so the per-lane spline uses ~1-ulp hardware forms:
 // squareplus from v_sqrt_f32 (no Newton step), quotients from a refined
 // reciprocal, and the log-det as ONE log of the product of its three terms
 // (2 log(sk+eps) + log(num2+eps) - 2 log(den+eps), utils.py:133-135).
 // Parity is checked by the same per-sample tolerance as every other path.
-#ifndef ZF_X3_FASTSPLINE
-#define ZF_X3_FASTSPLINE 1
-#endif
 __device__ __forceinline__ float x3_squareplus(float x) {
-#if ZF_X3_FASTSPLINE
   return 0.5f * (x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f)));
-#else
-  return squareplus_rsq(x);
-#endif
 }
 
 // 2*squareplus(x): the widths and heights are normalised by their sum, so the
 // factor 1/2 cancels exactly (a power of two): bit-identical knots.
 __device__ __forceinline__ float x3_squareplus2(float x) {
-#if ZF_X3_FASTSPLINE
   return x + __builtin_amdgcn_sqrtf(__builtin_fmaf(x, x, 4.0f));
-#else
-  return 2.0f * squareplus_rsq(x);
-#endif
 }
 
 __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
-#if ZF_X3_FASTSPLINE
   const float rw = rcp_refined(b.w);
   const float sk = b.h * rw;
   const float zr = (x - b.xk) * rw;  // :122
@@ -567,9 +512,6 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
   const float sq = (sk + kEps) * rd;
   const float l = __logf((num2 + kEps) * (sq * sq));
   ld = b.oob ? 0.0f : l;                                           // :138
-#else
-  rqs_forward_eval(x, b, y, ld);
-#endif
 }
 
 // Block: 4 waves x 32 samples, one 32-row input tile per weight group,
@@ -583,15 +525,12 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // parameter 32o + 16h + r), so it takes ceil((3K-1)/32) tiles instead of
 // ceil((3K-1)/16) half-empty ones, and the halves swap theirs by a lane
 // shuffle before the spline.
-#ifndef ZF_X3_NARROW_OCC
-#define ZF_X3_NARROW_OCC 3
-#endif
 // Waves per SIMD: hidden 128 with one dim pair and K <= 16 fits 168 VGPRs (3);
 // a dim-pair loop keeps the hidden activations live across the last layer,
 // and K = 32 holds 95 spline parameters per lane: 256 VGPRs (2); hidden 256
 // needs the whole register file (1).
 template <int T, int K, bool PAIRS>
-constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : ZF_X3_NARROW_OCC; }
+constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV>
 __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
@@ -659,7 +598,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // streamed layer (x3_step, SW) — except before a PAIRS last layer,
       // which passes over its input once per dim pair.
       constexpr bool kLastSW = !PAIRS;
-      constexpr bool kPipe = T == 4 && !PAIRS && ZF_X3_PIPE;
+      constexpr bool kPipe = T == 4 && !PAIRS;
       // f16x2: every layer leaves raw pre-activations; the next streamed
       // layer scales and swishes them (act_swish) as it goes.
       layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
@@ -667,10 +606,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
       // biases seed the accumulators.  f16x2: they seed them divided by the
       // unscale (exact: powers of two) and the accumulators are multiplied
-      // by it afterwards (kSeedScaled), or — ZF_X3_SEED_SCALED=0, hidden
-      // <= 128 — they join at the layer's end with the unscale in one fma
-      // (x3_finish; bias tiles live beside the accumulators there).
-      constexpr bool kSeedScaled = NT == 2 && (T == 8 || ZF_X3_SEED_SCALED);
+      // by it afterwards (kSeedScaled).
+      constexpr bool kSeedScaled = NT == 2;
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;

@@ -103,10 +103,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
   // summed pairwise at the end: a 256-long fp32 fma chain becomes four
   // 64-long ones (the input-gradient and forward GEMMs run K up to 256;
   // the weight-gradient chunks are 32 rows).
-#ifndef ZF_TRAIN_NACC
-#define ZF_TRAIN_NACC 4
-#endif
-  constexpr int NACC = (WG || TM * TN > 1) ? 1 : ZF_TRAIN_NACC;  // 128-wide tiles: registers for one set only
+  constexpr int NACC = (WG || TM * TN > 1) ? 1 : 4;  // 128-wide tiles: registers for one set only
   floatx16 acc[NACC][TM][TN];
 #pragma unroll
   for (int q = 0; q < NACC; ++q)
