@@ -62,7 +62,8 @@ def check_lp(lp, case, tag=""):
     both = fin32 & fin_gpu & np.isfinite(ref64)
     sens = O.row_sensitivity(case["model"], case["variables"], case["x"], case["c"])
     e_o32 = np.abs(ref32[both].astype(np.float64) - ref64[both])
-    allow = REL * scale[both] + 2 * (e_o32 + sens[both])
+    with np.errstate(over="ignore"):  # an overflowing row sensitivity just allows anything there
+        allow = REL * scale[both] + 2 * (e_o32 + sens[both])
     diff = np.abs(lp[both].astype(np.float64) - ref64[both])
     err = diff / scale[both]
     assert np.all(diff <= allow), f"{tag}: {np.sum(diff > allow)} rows over tolerance, max rel err {err.max():.3g}"
