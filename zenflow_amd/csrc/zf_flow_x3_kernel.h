@@ -608,6 +608,11 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // unscale (exact: powers of two) and the accumulators are multiplied
       // by it afterwards (kSeedScaled).
       constexpr bool kSeedScaled = NT == 2;
+      // Three waves share a SIMD at hidden 128: the one streaming weight
+      // groups (MFMAs) wins issue arbitration over one in its VALU-only
+      // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
+      // +1.2% d8; nothing to arbitrate at hidden 256, one wave per SIMD).
+      if constexpr (T == 4) __builtin_amdgcn_s_setprio(2);
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;
@@ -682,6 +687,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
           for (int o = 0; o < TL; ++o) pa[o] *= lus;
         }
+        if constexpr (T == 4) __builtin_amdgcn_s_setprio(0);
         float P[NPV];
 #pragma unroll
         for (int o = 0; o < TL; ++o)
