@@ -55,7 +55,16 @@ WORKLOADS = {
     # knots 16, layers (128, 128)), and K = 32 at hidden 128
     "d8": (8, 0, 16, (128, 128), 8, "normal", "log_prob"),
     "d4k32": (4, 0, 32, (128, 128), 4, "normal", "log_prob"),
+    # cfg2 with NeuralSplineCoupling(act=...) other than swish (bijectors.py:319)
+    "cfg2relu": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "relu"),
+    "cfg2gelu": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "gelu"),
 }
+
+
+def workload(name):
+    """(D, C, K, layers, couplings, latent, mode, act) of a bench workload."""
+    w = WORKLOADS[name]
+    return tuple(w[:7]) + ((w[7] if len(w) > 7 else "swish"),)
 
 
 def build_model(name):
@@ -63,18 +72,18 @@ def build_model(name):
     from zenflow_amd import bijectors as bi
     from zenflow_amd import distributions as dist
 
-    D, C, K, layers, L, latent, mode = WORKLOADS[name]
+    D, C, K, layers, L, latent, mode, act = workload(name)
     bij = [bi.ShiftBounds(margin=0.1)]
     for _ in range(L - 1):
-        bij += [bi.NeuralSplineCoupling(knots=K, layers=layers), bi.Roll()]
-    bij.append(bi.NeuralSplineCoupling(knots=K, layers=layers))
+        bij += [bi.NeuralSplineCoupling(knots=K, layers=layers, act=act), bi.Roll()]
+    bij.append(bi.NeuralSplineCoupling(knots=K, layers=layers, act=act))
     lat = dist.Normal() if latent == "normal" else dist.Beta()
     return zf.Flow(bi.Chain(bij), latent=lat)
 
 
 def flops_per_sample(name):
     """2 * MACs of the conditioner MLPs: 2*L*[(dc+C)H + H*H + H*dt*S]."""
-    D, C, K, layers, L, _, _ = WORKLOADS[name]
+    D, C, K, layers, L, _, _, _ = workload(name)
     dt, dc = D // 2, D - D // 2
     widths = [dc + C] + list(layers) + [dt * (3 * K - 1)]
     return 2 * L * sum(a * b for a, b in zip(widths[:-1], widths[1:]))
@@ -186,11 +195,11 @@ def spline_kernel_roofline(M, N, K, steps):
 
 
 def oracle_spec(name):
-    D, C, K, layers, L, latent, _ = WORKLOADS[name]
+    D, C, K, layers, L, latent, _, act = workload(name)
     bij = [{"type": "shift_bounds", "margin": 0.1, "bounds": ()}]
     for _ in range(L - 1):
-        bij += [{"type": "nsc", "knots": K, "layers": list(layers)}, {"type": "roll", "shift": 1}]
-    bij.append({"type": "nsc", "knots": K, "layers": list(layers)})
+        bij += [{"type": "nsc", "knots": K, "layers": list(layers), "act": act}, {"type": "roll", "shift": 1}]
+    bij.append({"type": "nsc", "knots": K, "layers": list(layers), "act": act})
     return {"bijector": {"type": "chain", "bijectors": bij}, "latent": {"type": latent}}
 
 
@@ -248,7 +257,7 @@ def main():
 
     L.ensure_device()
     name = args.config
-    D, C, K, layers, nL, latent, mode = WORKLOADS[name]
+    D, C, K, layers, nL, latent, mode, act = workload(name)
     N = 1 << (args.rows_log2 if args.rows_log2 is not None else (12 if mode == "apply" else 20))
     flow = build_model(name)
     # Random-init weights of the named architecture (flax default initialisers),
@@ -347,7 +356,8 @@ def main():
         "data": "synthetic: x ~ N(0, I) per rank; random-init weights (flax default initialisers) "
                 "+ one train-mode pass for ShiftBounds/BatchNorm statistics",
         "config": {
-            "workload": f"{name}: Flow(rolling_spline_coupling({D}, knots={K}, layers={list(layers)})"
+            "workload": f"{name}: Flow(rolling_spline_coupling({D}, knots={K}, layers={list(layers)}"
+            + ("" if act == "swish" else f", act={act}") + ")"
                         f"{' x' + str(nL) + ' couplings' if nL != D else ''}, latent={latent}).{mode}, "
                         f"{N} rows per GPU, resident in HBM",
             "rows_per_gpu": N,

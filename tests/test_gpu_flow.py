@@ -73,7 +73,7 @@ def check_lp(lp, case, tag=""):
 
 
 WIDE_SHAPES = ["d6", "d8", "d16", "d7k32c2", "d4k32", "d3k32", "d4h256k8", "d5h64"]
-from tests.flowcases import ACTS  # noqa: E402  (NeuralSplineCoupling.act other than swish: fp32 kernel)
+from tests.flowcases import ACTS  # noqa: E402  (NeuralSplineCoupling.act other than swish)
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"]
@@ -270,19 +270,23 @@ def test_golden_edges(name):
 # the fp32-MFMA kernel, which must stay parity-green on the same shapes.
 
 X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
+X3_ACTS = [a for a in ACTS if a not in ("sigmoid", "softplus")]
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"] + ACTS)
 def test_kernel_selection(name, monkeypatch):
+    """relu, leaky_relu, tanh, gelu and elu run on f16x2 (its activation
+    switch); sigmoid and softplus, and every other activation under the
+    bf16x3 scheme, on the fp32 kernel (x3_eligible)."""
     case = make_case(name, N=8, seed=30)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == ("f16x2" if name in X3_SHAPES else "fp32")
+    assert bf.program.kernel_variant == ("f16x2" if name in X3_SHAPES + X3_ACTS else "fp32")
     monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
     _, bf = _bound(case)
     assert bf.program.kernel_variant == ("bf16x3" if name in X3_SHAPES else "fp32")
 
 
-@pytest.mark.parametrize("name", X3_SHAPES)
+@pytest.mark.parametrize("name", X3_SHAPES + ACTS)
 def test_fp32_kernel_parity_when_x3_disabled(name, monkeypatch):
     monkeypatch.setenv("ZF_DISABLE_X3", "1")
     case = make_case(name, N=3000, seed=31)
@@ -329,6 +333,32 @@ def test_split_scaling_extremes(scheme, name, regime, monkeypatch):
     _, bf = _bound(case)
     assert bf.program.kernel_variant == scheme
     check_lp(gpu_log_prob(case), case, f"{scheme}/{name}/{regime}")
+
+
+@pytest.mark.parametrize("name", X3_ACTS)
+@pytest.mark.parametrize("regime", ["huge_activations", "tiny_activations", "tiny_weights", "huge_weights"])
+def test_split_scaling_extremes_other_acts(name, regime):
+    """The same magnitude regimes on the f16x2 activation switch (every
+    activation it takes is bounded by |v|, x3_act_scale)."""
+    case = make_case(name, N=1500, seed=36)
+    params = case["variables"]["params"]["bijector"]
+    for key, p in params.items():
+        if regime == "huge_activations":
+            p["BatchNorm_0"]["scale"] = (p["BatchNorm_0"]["scale"] * 3e3).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-3).astype(F32)
+        elif regime == "tiny_activations":
+            p["Dense_0"]["kernel"] = (p["Dense_0"]["kernel"] * 1e-6).astype(F32)
+            p["Dense_0"]["bias"] = (p["Dense_0"]["bias"] * 1e-6).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e4).astype(F32)
+        elif regime == "tiny_weights":
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-7).astype(F32)
+        else:
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e5).astype(F32)
+            last = f"Dense_{len(case['cfg']['layers'])}"
+            p[last]["kernel"] = (p[last]["kernel"] * 1e-5).astype(F32)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "f16x2"
+    check_lp(gpu_log_prob(case), case, f"{name}/{regime}")
 
 
 @pytest.mark.parametrize("N", [255, 256, 257, 129, 100003])

@@ -384,6 +384,7 @@ struct zf_flow {
   float* d_blob = nullptr;
   void* d_x3 = nullptr;       // bf16x3 weight-group stream (x3 kernel), or null
   int x3_K = 0;
+  bool x3_oact = false;  // some coupling's activation is not swish
   int device = 0;
 };
 
@@ -606,6 +607,8 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
     zf::x3_pack(desc, nat, T, NT, F, P, x3s);
     F.x3_ok = NT == 3 ? 1 : 2;
     h->x3_K = x3K;
+    for (int i = 0; i < desc.n_ops; ++i)
+      if (desc.ops[i].kind == ZF_OP_NSC && desc.ops[i].act != ZF_ACT_SWISH) h->x3_oact = true;
   }
   const bool use_x3 = F.x3_ok != 0;
   int rcd = ZF_OK;
@@ -668,6 +671,7 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
     a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.T = h->host.HP / 32;
     a.NT = h->host.x3_ok == 2 ? 2 : 3;
+    a.oact = h->x3_oact;
     a.seed = seed;
     a.gen = gen;
     a.stream = (hipStream_t)stream;

@@ -314,6 +314,7 @@ struct X3Launch {
   int gen;  // 1: draw the input rows from the latent (zf_flow_sample)
   int K, D, T;  // knots, dim, hidden tiles (4: width <= 128, 8: <= 256)
   int NT;       // split scheme: 3 = bf16x3, 2 = f16x2
+  bool oact;    // some coupling's activation is not swish (f16x2 kernels with act switch)
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);

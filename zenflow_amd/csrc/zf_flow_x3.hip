@@ -44,7 +44,16 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind != ZF_OP_NSC) continue;
-    if (op.act != ZF_ACT_SWISH) return false;  // the split kernel fuses swish only
+    // Activations other than swish: f16x2 only (the bf16x3 reference scheme
+    // keeps swish), and only those with act(0) = 0 and |act(v)| <= |v|
+    // (relu, leaky_relu, tanh, gelu, elu): the per-sample power-of-two scale
+    // then keeps every value's relative precision.  sigmoid and softplus
+    // carry their information as small deviations from 1/2 and log 2, which
+    // 22-bit split operands resolve worse than fp32 (measured: 1e-3 relative
+    // on tiny pre-activations amplified by large weights); they stay on the
+    // fp32 kernel.
+    const int a = op.act;
+    if (a != ZF_ACT_SWISH && (x3_scheme() != 2 || a == ZF_ACT_SIGMOID || a == ZF_ACT_SOFTPLUS)) return false;
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }
@@ -97,12 +106,14 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
       const int out = last ? dt * S : op.hidden[l];
       const int NOUT = last ? TL : T;
       const float* W = nat + op.off_w[l];
+      // f16x2: the inputs of swished layers' activations carry log2(e)
+      const float pre = (NT == 2 && !last && op.act == ZF_ACT_SWISH) ? kSwishPrescale : 1.0f;
       // f16x2: the layer's power-of-two scale, max |W| * 2^kw in [2^13, 2^14)
       int kw = 0;
       if (NT == 2) {
         float mx = 0.f;
         for (int64_t i = 0; i < (int64_t)in * out; ++i)
-          mx = std::fmax(mx, std::fabs(W[i] * (last ? 1.0f : kSwishPrescale)));
+          mx = std::fmax(mx, std::fabs(W[i] * pre));
         if (mx > 0.f && std::isfinite(mx)) {
           int e;
           std::frexp(mx, &e);
@@ -110,7 +121,6 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
         }
       }
       d.x3_kw[l] = kw;
-      const float pre = (NT == 2 && !last) ? kSwishPrescale : 1.0f;
       for (int pr = 0; pr < (last ? NP : 1); ++pr)
         for (int q = 0; q < T; ++q)
           for (int s = 0; s < 2; ++s)
@@ -153,8 +163,9 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
             }
     }
     // f16x2: Dense_0 (fp32 fragments, d.w[0]) and the hidden biases of the
-    // swished layers join the log2(e) prescale (act_swish).
-    if (NT == 2) {
+    // swished layers join the log2(e) prescale (act_swish); other
+    // activations take their pre-activations unscaled.
+    if (NT == 2 && op.act == ZF_ACT_SWISH) {
       const int KS0 = d.KS0;
       for (int64_t i = 0; i < (int64_t)T * KS0 * 64; ++i) packed[d.w[0] + i] *= kSwishPrescale;
       for (int l = 0; l < op.n_hidden; ++l)

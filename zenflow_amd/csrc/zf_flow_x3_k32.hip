@@ -4,7 +4,10 @@
 
 namespace zf {
 
+int launch_x3_k32_act(const X3Launch& a, bool inverse);
+
 int launch_x3_k32(const X3Launch& a, bool inverse) {
+  if (a.oact) return launch_x3_k32_act(a, inverse);
   return a.NT == 2 ? launch_x3_k<2, 32>(a, inverse) : launch_x3_k<3, 32>(a, inverse);
 }
 

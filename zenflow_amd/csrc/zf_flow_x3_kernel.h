@@ -165,6 +165,38 @@ __device__ __forceinline__ float act_swish(float v, float c) {
   return swish(v);
 }
 
+// The layer-input activation of one accumulator tile.  OACT = false: every
+// coupling is swish (act_swish, the tuned form).  OACT = true (f16x2 only):
+// NeuralSplineCoupling.act per coupling (wave-uniform `act`, zf_act.h forms,
+// one switch per tile); swish couplings keep act_swish and the log2(e)
+// prescale, the others are packed unscaled and multiply their activation by
+// the power-of-two scale c = sc of x3_act_scale.
+template <int CODE>
+__device__ __forceinline__ void act_tile_fixed(floatx16& t, float c) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] = act_other(CODE, t[r]) * c;
+}
+
+template <int NT, bool OACT>
+__device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
+  if constexpr (!OACT) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+  } else {
+    static_assert(NT == 2, "other activations run on the f16x2 scheme");
+    switch (act) {
+      case ZF_ACT_RELU: act_tile_fixed<ZF_ACT_RELU>(t, c); break;
+      case ZF_ACT_TANH: act_tile_fixed<ZF_ACT_TANH>(t, c); break;
+      case ZF_ACT_GELU: act_tile_fixed<ZF_ACT_GELU>(t, c); break;
+      case ZF_ACT_ELU: act_tile_fixed<ZF_ACT_ELU>(t, c); break;
+      case ZF_ACT_LEAKY_RELU: act_tile_fixed<ZF_ACT_LEAKY_RELU>(t, c); break;
+      default:
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+    }
+  }
+}
+
 __device__ __forceinline__ floatx16 mfma3(const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                           const bf16x8& bh, const bf16x8& bm, const bf16x8& bl,
                                           floatx16 acc) {
@@ -205,18 +237,23 @@ __device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)
 // scales on the accumulator: us = 2^-(e_act + kw) (ius = 1/us).  Returned
 // in isc: the swish constant c = isc*log2(e) (act_swish).  Lanes l and l^32
 // hold the same sample.
-template <int T>
-__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius) {
+template <int T, bool OACT = false>
+__device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius,
+                                             int act = ZF_ACT_SWISH) {
   float m = 0.f;
 #pragma unroll
   for (int t = 0; t < T; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
   m = fmaxf(m, __shfl_xor(m, 32));
+  // OACT: |act(v)| <= |v| for every activation the kernel takes (relu,
+  // leaky_relu, tanh, gelu, elu; x3_eligible), so the bound holds as for swish.
   // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
   // seeded as bias / us stays finite)
   const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
-  isc = __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
+  // swish: the act_swish constant c = 2^(e-14) log2(e); others: sc = 2^(14-e)
+  isc = (OACT && act != ZF_ACT_SWISH) ? __builtin_amdgcn_ldexpf(1.0f, 14 - e)
+                                      : __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
   us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
   ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
 }
@@ -363,10 +400,10 @@ __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const
 // a layer whose accumulators did not start from the bias, loaded here — in
 // the layer's last step, when its earlier input tiles are dead — and joined
 // after the MFMAs (x3_finish, which also undoes the f16x2 scales).
-template <int NT, int T, int NOUT, int Q, bool SW>
+template <int NT, int T, int NOUT, int Q, bool SW, bool OACT>
 __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                        int hh, float isc, float us) {
+                                        int hh, float isc, float us, int act) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
@@ -384,8 +421,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   // of tile Q+1 goes here, in the same scheduling region as this group's
   // MFMAs, whose issue gaps it fills.
   if constexpr (SW && Q + 1 < T) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+    x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
   }
   if constexpr (T == 8) {
     // the k-step-0 split first, then every MFMA followed by its share of LDS
@@ -412,10 +448,11 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 // (Q+1, 0) for the next group — so the bf16 split and the deferred swish sit
 // in the MFMA issue gaps of the same wave (cross-wave they would not overlap:
 // tests/hip/coexec_probe.hip modes 2 and 6).
-template <int NT, int T, int NOUT, int Q, bool HASB>
+template <int NT, int T, int NOUT, int Q, bool HASB, bool OACT>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                             int hh, typename XT<NT>::E (&cs)[NT], float isc, float us) {
+                                             int hh, typename XT<NT>::E (&cs)[NT], float isc, float us,
+                                             int act) {
   using E = typename XT<NT>::E;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -435,8 +472,7 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
     acc[o] = mfma_split<NT>(a, cs, acc[o]);
   }
   if constexpr (Q + 1 < T) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+    x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
     splitk<NT, 0>(hb[Q + 1], cs);
   }
 #pragma unroll
@@ -456,28 +492,28 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 }
 
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
-template <int NT, int T, int NOUT, bool HASB, int Q = 0>
+template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                              typename XT<NT>::E (&cs)[NT], float isc, float us) {
+                                              typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
   if constexpr (Q + 1 < T) {
-    x3_step_pipe<NT, T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us);
-    x3_layer_pipe<NT, T, NOUT, HASB, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+    x3_step_pipe<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
+    x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   } else {
-    x3_step_pipe<NT, T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+    x3_step_pipe<NT, T, NOUT, Q, HASB, OACT>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   }
 }
 
 // A whole streamed Dense layer: T groups (one per input tile).
-template <int NT, int T, int NOUT, bool SW, int Q = 0>
+template <int NT, int T, int NOUT, bool SW, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                          floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                         float isc, float us) {
+                                         float isc, float us, int act) {
   if constexpr (Q + 1 < T) {
-    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, nullptr, hh, isc, us);
-    x3_layer<NT, T, NOUT, SW, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
+    x3_step<NT, T, NOUT, Q, SW, OACT>(x3, p, hb, acc, lane, nullptr, hh, isc, us, act);
+    x3_layer<NT, T, NOUT, SW, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, isc, us, act);
   } else {
-    x3_step<NT, T, NOUT, Q, SW>(x3, p, hb, acc, lane, bias_last, hh, isc, us);
+    x3_step<NT, T, NOUT, Q, SW, OACT>(x3, p, hb, acc, lane, bias_last, hh, isc, us, act);
   }
 }
 
@@ -528,12 +564,14 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // Waves per SIMD: hidden 128 with one dim pair and K <= 16 fits 168 VGPRs (3);
 // a dim-pair loop keeps the hidden activations live across the last layer,
 // and K = 32 holds 95 spline parameters per lane: 256 VGPRs (2); hidden 256
-// needs the whole register file (1).
+// needs the whole register file (1).  The activation switch of OACT
+// kernels (one branch per tile inside the pipelined steps) needs the
+// 2-wave budget too (at 3 it spilled 110-130 VGPRs).
 template <int T, int K, bool PAIRS>
 constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
 
-template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV>
-__global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT>
+__global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS || OACT>())) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
@@ -617,9 +655,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;
         if constexpr (NT == 2) {
-          x3_act_scale<T>(hb, op.x3_kw[l], isc, us, ius);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) hb[0][r] = act_swish<NT>(hb[0][r], isc);
+          x3_act_scale<T, OACT>(hb, op.x3_kw[l], isc, us, ius, op.act);
+          x3_act_tile<NT, OACT>(hb[0], isc, op.act);
         }
 #pragma unroll
         for (int o = 0; o < T; ++o)
@@ -629,9 +666,10 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
-          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us);
+          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
+                                                                 op.act);
         } else {
-          x3_layer<NT, T, T, true>(x3, pipe, hb, acc, lane, bh, hh, isc, us);
+          x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, op.act);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
@@ -657,13 +695,11 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       const int npair = PAIRS ? (dt + 1) / 2 : 1;
       float lisc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
       if constexpr (NT == 2) {
-        x3_act_scale<T>(hb, op.x3_kw[op.n_hidden], lisc, lus, lius);
+        x3_act_scale<T, OACT>(hb, op.x3_kw[op.n_hidden], lisc, lus, lius, op.act);
         // PAIRS: the input is read once per dim pair, so swish it whole here
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          if (o == 0 || !kLastSW)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) hb[o][r] = act_swish<NT>(hb[o][r], lisc);
+          if (o == 0 || !kLastSW) x3_act_tile<NT, OACT>(hb[o], lisc, op.act);
       }
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
@@ -679,9 +715,10 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
-          x3_layer_pipe<NT, T, TL, !kSeedScaled>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus);
+          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, op.act);
         } else {
-          x3_layer<NT, T, TL, kLastSW>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh, lisc, lus);
+          x3_layer<NT, T, TL, kLastSW, OACT>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh,
+                                             lisc, lus, op.act);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
@@ -758,7 +795,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
                     ld_out, s_part);
 }
 
-template <int NT, int K, int T, bool PAIRS, bool ONE>
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool OACT>
 int launch_x3(const X3Launch& a, bool inverse) {
   const long long rows = kX3Waves * kTile;
   const long long grid = (a.N + rows - 1) / rows;
@@ -767,11 +804,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
   const size_t lds = x3_lds_bytes(T > TL ? T : TL, a.D, NT);
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true, OACT>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false, OACT>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
@@ -782,16 +819,18 @@ int launch_x3(const X3Launch& a, bool inverse) {
 // and hidden 256 (T = 8).  PAIRS (a loop over transformed-dim pairs in the
 // last layer) whenever dt > 2, and always at T = 8 (its hidden activations
 // are live across the last layer anyway); ONE when dt == 1.
-template <int NT, int K>
+// OACT: some coupling's activation is not swish (f16x2 only).
+template <int NT, int K, bool OACT = false>
 int launch_x3_k(const X3Launch& a, bool inverse) {
   const int dt = a.D / 2;
   const bool one = dt == 1;  // must match x3_pack's last-layer layout
   if (a.T == 4) {
-    if (dt > 2) return launch_x3<NT, K, 4, true, false>(a, inverse);
-    return one ? launch_x3<NT, K, 4, false, true>(a, inverse) : launch_x3<NT, K, 4, false, false>(a, inverse);
+    if (dt > 2) return launch_x3<NT, K, 4, true, false, OACT>(a, inverse);
+    return one ? launch_x3<NT, K, 4, false, true, OACT>(a, inverse)
+               : launch_x3<NT, K, 4, false, false, OACT>(a, inverse);
   }
   if (a.T == 8)
-    return one ? launch_x3<NT, K, 8, true, true>(a, inverse) : launch_x3<NT, K, 8, true, false>(a, inverse);
+    return one ? launch_x3<NT, K, 8, true, true, OACT>(a, inverse) : launch_x3<NT, K, 8, true, false, OACT>(a, inverse);
   return enotsup("split-MFMA kernel: hidden tiles not instantiated");
 }
 
