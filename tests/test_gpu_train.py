@@ -255,3 +255,27 @@ def test_step_graph_matches_eager(monkeypatch):
     assert flat[0].keys() == flat[1].keys()
     for k in flat[0]:
         np.testing.assert_array_equal(flat[0][k], flat[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("name,N,seed", [("cfg2", 1024, 66), ("d2h256", 2048, 67), ("gelu", 512, 68)])
+def test_split_set_gemm_matches_single_kernel(name, N, seed, monkeypatch):
+    """Small batches run the 64x64 GEMM tiles as four blocks, one per
+    accumulator set of the interleaved kernel, plus a combine (SPLITQ in
+    zf_train.hip): the same loss, gradient and trained parameters, bit for
+    bit, as the single-kernel form (ZF_TRAIN_SPLITQ=0)."""
+    from zenflow_amd import _lib as L
+
+    out = []
+    for sq in ("1", "0"):
+        monkeypatch.setenv("ZF_TRAIN_SPLITQ", sq)
+        case, flow, tr = _setup(name, N, seed)
+        loss, g = tr.loss_grad(case["x"], case["c"])
+        for _ in range(2):
+            tr.step(case["x"], case["c"])
+        blob = np.empty_like(tr.program.blob)
+        L.check(L.load_library().zf_trainer_get_blob(tr.handle, blob.ctypes.data), "get_blob")
+        out.append((loss, g, tr.last_loss(), blob))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1]), f"{np.sum(out[0][1] != out[1][1])} gradient entries differ"
+    assert out[0][2] == out[1][2]
+    assert np.array_equal(out[0][3], out[1][3], equal_nan=True)

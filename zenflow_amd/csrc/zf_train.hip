@@ -54,7 +54,31 @@ enum { kEpiNone = 0, kEpiBias = 1, kEpiDSwish = 2 };
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
 
-template <int BM, int BN, bool TA, bool TB, bool WG>
+// The fused store of one output element (both GEMM forms below).
+__device__ __forceinline__ void gemm_epilogue(float v, int n, long long o, float* __restrict__ C, int epi,
+                                              const float* __restrict__ bias, float* __restrict__ H,
+                                              const float* __restrict__ Z, int act) {
+  if (epi == kEpiBias) {
+    v = v + bias[n];
+    if (H) H[o] = act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
+  } else if (epi == kEpiDSwish) {
+    const float z = Z[o];
+    if (act == ZF_ACT_SWISH) {
+      const float sg = sigmoidf(z);
+      v = v * (sg + z * sg * (1.0f - sg));
+    } else {
+      v = v * act_other_grad(act, z);
+    }
+  }
+  C[o] = v;
+}
+
+// SPLITQ: block z = q of a 64 x 64 tile multiplies only the k-pairs
+// p = q (mod 4) — exactly accumulator set q of the NACC = 4 kernel, in the
+// same order — into part[q][M][N]; gemm_combine_kernel then forms
+// (P0 + P1) + (P2 + P3) and the epilogue: the same bits from four times the
+// blocks (small batches: 1024 rows give 32 tiles for 256 CUs).
+template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
 __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                     int ldc, int epi, const float* __restrict__ bias,
@@ -103,7 +127,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
   // summed pairwise at the end: a 256-long fp32 fma chain becomes four
   // 64-long ones (the input-gradient and forward GEMMs run K up to 256;
   // the weight-gradient chunks are 32 rows).
-  constexpr int NACC = (WG || TM * TN > 1) ? 1 : 4;  // 128-wide tiles: registers for one set only
+  constexpr int NACC = (WG || SPLITQ || TM * TN > 1) ? 1 : 4;  // 128-wide tiles: registers for one set only
   floatx16 acc[NACC][TM][TN];
 #pragma unroll
   for (int q = 0; q < NACC; ++q)
@@ -122,8 +146,10 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
     store();
     __syncthreads();
     if (k0 + MBK < kend) load(k0 + MBK);
+    const int kq = SPLITQ ? 2 * (int)blockIdx.z : 0;
 #pragma unroll
-    for (int kb = 0; kb < MBK; kb += 2) {
+    for (int kb0 = 0; kb0 < MBK; kb0 += SPLITQ ? 8 : 2) {
+      const int kb = kb0 + kq;
       float a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) a[i] = As[kb + h][wm0 + 32 * i + r];
@@ -149,6 +175,15 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
       for (int j = 0; j < TN; ++j)
         acc[0][i][j] = NACC == 4 ? (acc[0][i][j] + acc[1][i][j]) + (acc[2][i][j] + acc[3][i][j])
                                  : acc[0][i][j] + acc[1][i][j];
+  }
+  if (SPLITQ) {
+    float* P = C + (long long)blockIdx.z * M * N;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int m = m0 + wm0 + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + r;
+      if (m < M && n < N) P[(long long)m * N + n] = acc[0][0][0][q];
+    }
+    return;
   }
   if (WG) {
     float* P = C + (long long)blockIdx.z * (M + 1) * N;
@@ -180,24 +215,47 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-        if (m < M && n < N) {
-          const long long o = (long long)m * ldc + n;
-          float v = acc[0][i][j][q];
-          if (epi == kEpiBias) {
-            v = v + bias[n];
-            if (H) H[o] = act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
-          } else if (epi == kEpiDSwish) {
-            const float z = Z[o];
-            if (act == ZF_ACT_SWISH) {
-              const float sg = sigmoidf(z);
-              v = v * (sg + z * sg * (1.0f - sg));
-            } else {
-              v = v * act_other_grad(act, z);
-            }
-          }
-          C[o] = v;
-        }
+        if (m < M && n < N) gemm_epilogue(acc[0][i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
       }
+}
+
+__global__ void gemm_combine_kernel(int M, int N, const float* __restrict__ P, float* __restrict__ C, int ldc,
+                                    int epi, const float* __restrict__ bias, float* __restrict__ H,
+                                    const float* __restrict__ Z, int act) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long MN = (long long)M * N;
+  if (i >= MN) return;
+  const int m = (int)(i / N), n = (int)(i - (long long)m * N);
+  const float v = (P[i] + P[MN + i]) + (P[2 * MN + i] + P[3 * MN + i]);
+  gemm_epilogue(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+}
+
+// C = A . B for K <= 8 (the first Dense of a coupling: K = dc + C inputs),
+// one thread per output, with the arithmetic of the 64 x 64 interleaved
+// MFMA kernel: k-pair p into set p mod 4 as fma(a1, b1, fma(a0, b0, s)) (the
+// f32 MFMA's k-ordered fma chain), the tile's all-zero pairs as s + 0 (they
+// only turn -0 into +0), then (s0 + s1) + (s2 + s3) and the same epilogue.
+// The MFMA kernel would run 32 blocks of one mostly empty k-tile.
+__global__ void gemm_small_k_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                    const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc, int epi,
+                                    const float* __restrict__ bias, float* __restrict__ H,
+                                    const float* __restrict__ Z, int act) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (long long)m * N);
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = 2 * p;
+    if (k < K) {
+      const float a0 = A[(long long)m * lda + k], b0 = B[(long long)k * ldb + n];
+      const float a1 = k + 1 < K ? A[(long long)m * lda + k + 1] : 0.f;
+      const float b1 = k + 1 < K ? B[(long long)(k + 1) * ldb + n] : 0.f;
+      sq[p] = __builtin_fmaf(a1, b1, __builtin_fmaf(a0, b0, sq[p]));
+    }
+  }
+  const float v = (__fadd_rn(sq[0], 0.f) + __fadd_rn(sq[1], 0.f)) + (__fadd_rn(sq[2], 0.f) + __fadd_rn(sq[3], 0.f));
+  gemm_epilogue(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
 }
 
 template <int T>
@@ -216,14 +274,38 @@ void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const fl
 // least 512 blocks over the GLOBAL batch's Mg rows, 64 x 64 otherwise.  The
 // two tiles accumulate differently (one chain vs four interleaved), so the
 // choice follows the global batch: every data-parallel shard then runs the
-// kernel, and gets the bits, of the one-device step.
+// kernel, and gets the bits, of the one-device step.  64 x 64 tiles that
+// would leave most CUs idle (< 256 blocks, K >= 64) run as the four split
+// sets + combine (SPLITQ; same bits) when a workspace of 4 M N floats is
+// given (`split`, the trainer's split-K buffer), and K <= 8 as one thread
+// per output (gemm_small_k_kernel; same bits); ZF_TRAIN_SPLITQ=0: neither.
 int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
          int ldc, hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
-         const float* Z = nullptr, int act = ZF_ACT_SWISH) {
+         const float* Z = nullptr, int act = ZF_ACT_SWISH, float* split = nullptr, long long split_cap = 0) {
   if (M <= 0 || N <= 0) return ZF_OK;
   const long long big = (long long)((N + 127) / 128) * ((Mg + 127) / 128);
-  if (big >= 512) gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
-  else gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
+  const long long tiles64 = (long long)((N + 63) / 64) * ((M + 63) / 64);
+  if (big >= 512) {
+    gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
+  } else if (split != nullptr && !tb && K <= 8) {
+    const long long MN = (long long)M * N;
+    hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, epi, bias, H, Z, act);
+  } else if (split != nullptr && tiles64 < 256 && K >= 64 && 4ll * M * N <= split_cap) {
+    const dim3 grid((N + 63) / 64, (M + 63) / 64, 4);
+    if (!tb)
+      hipLaunchKernelGGL((mgemm_kernel<64, 64, false, false, false, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B,
+                         ldb, split, N, kEpiNone, nullptr, nullptr, nullptr, 0, act);
+    else
+      hipLaunchKernelGGL((mgemm_kernel<64, 64, false, true, false, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B,
+                         ldb, split, N, kEpiNone, nullptr, nullptr, nullptr, 0, act);
+    ZF_CHECK_LAUNCH("mgemm_kernel<splitq>");
+    const long long MN = (long long)M * N;
+    hipLaunchKernelGGL(gemm_combine_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, split, C, ldc,
+                       epi, bias, H, Z, act);
+  } else {
+    gemm_launch<64>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
+  }
   ZF_CHECK_LAUNCH("mgemm_kernel");
   return ZF_OK;
 }
@@ -1034,6 +1116,7 @@ struct zf_trainer {
   std::map<int64_t, hipGraphExec_t> graphs;
   bool use_graph = true;
   bool bn_small = true;  // ZF_TRAIN_BN_SMALL=0: always the multi-launch BatchNorm path
+  bool splitq = true;    // ZF_TRAIN_SPLITQ=0: never the split-set GEMM (same bits either way)
   float* d_ld = nullptr;      // [bmax]
   float* d_g0 = nullptr;      // [bmax][D]
   float* d_g1 = nullptr;
@@ -1148,6 +1231,8 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
     t->use_graph = !(g && g[0] == '0');
     const char* bs = std::getenv("ZF_TRAIN_BN_SMALL");
     t->bn_small = !(bs && bs[0] == '0');
+    const char* sq = std::getenv("ZF_TRAIN_SPLITQ");
+    t->splitq = !(sq && sq[0] == '0');
   }
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&t->cap, hipStreamNonBlocking);
@@ -1339,7 +1424,8 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         const int out_w = last ? dt * S : op.hidden[l];
         float* Z = last ? nb.P : nb.Z[l];
         rc = zf::gemm(false, Bg, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
-                      nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act);
+                      nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act, t->splitq ? t->d_ws : nullptr,
+                      zf::kWsFloats);
         if (rc) return rc;
         if (!last) {
           in = nb.H[l];
@@ -1410,7 +1496,8 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       float* gin = l == 0 ? nb.gU : gbufs[which];
       // (through swish of layer l-1 when l > 0)
       rc = zf::gemm(true, Bg, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
-                    l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act);
+                    l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act,
+                    t->splitq ? t->d_ws : nullptr, zf::kWsFloats);
       if (rc) return rc;
       if (l > 0) {
         gout = gin;
