@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-tuning builds: ab/lib<name>.so for each "name=extra hipcc flags" argument,
-# all from the working tree (e.g. base= sched2=-DZF_X3_SCHED=2).
+# all from the working tree (e.g. base= noslp=-fno-slp-vectorize).
 set -eu
 cd "$(dirname "$0")/.."
 mkdir -p ab
