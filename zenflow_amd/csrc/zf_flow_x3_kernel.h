@@ -420,7 +420,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   // SW: the layer input arrives as pre-activations except tile 0; the swish
   // of tile Q+1 goes here, in the same scheduling region as this group's
   // MFMAs, whose issue gaps it fills.
-  if constexpr (SW && Q + 1 < T) {
+  if constexpr (SW && !OACT && Q + 1 < T) {
     x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
   }
   if constexpr (T == 8) {
@@ -472,7 +472,7 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
     acc[o] = mfma_split<NT>(a, cs, acc[o]);
   }
   if constexpr (Q + 1 < T) {
-    x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
+    if constexpr (!OACT) x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
     splitk<NT, 0>(hb[Q + 1], cs);
   }
 #pragma unroll
@@ -564,14 +564,14 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // Waves per SIMD: hidden 128 with one dim pair and K <= 16 fits 168 VGPRs (3);
 // a dim-pair loop keeps the hidden activations live across the last layer,
 // and K = 32 holds 95 spline parameters per lane: 256 VGPRs (2); hidden 256
-// needs the whole register file (1).  The activation switch of OACT
-// kernels (one branch per tile inside the pipelined steps) needs the
-// 2-wave budget too (at 3 it spilled 110-130 VGPRs).
+// needs the whole register file (1).  OACT kernels apply the activation to
+// all tiles before the layer's groups instead of tile by tile inside them
+// (a switch inside the pipelined steps spilled 110-130 VGPRs at 3 waves).
 template <int T, int K, bool PAIRS>
 constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT>
-__global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS || OACT>())) void flow_kernel_x3(
+__global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
     const float* __restrict__ ld_in, float* __restrict__ ld_out, float* __restrict__ lp_out,
@@ -656,7 +656,10 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS || OACT>()
         float isc = 1.f, us = 1.f, ius = 1.f;
         if constexpr (NT == 2) {
           x3_act_scale<T, OACT>(hb, op.x3_kw[l], isc, us, ius, op.act);
-          x3_act_tile<NT, OACT>(hb[0], isc, op.act);
+          // OACT: every tile here, outside the MFMA stream (the switch there
+          // would cost a third of the waves)
+#pragma unroll
+          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT>(hb[o], isc, op.act);
         }
 #pragma unroll
         for (int o = 0; o < T; ++o)
@@ -699,7 +702,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS || OACT>()
         // PAIRS: the input is read once per dim pair, so swish it whole here
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          if (o == 0 || !kLastSW) x3_act_tile<NT, OACT>(hb[o], lisc, op.act);
+          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT>(hb[o], lisc, op.act);
       }
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
