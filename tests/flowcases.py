@@ -37,7 +37,8 @@ CONFIGS = {
     "d4h256k8": dict(D=4, C=1, K=8, layers=(256, 256), latent="normal"),
     "d5h64": dict(D=5, C=0, K=16, layers=(64, 64), latent="normal"),
     # NeuralSplineCoupling(act=...) other than swish (bijectors.py:319): the
-    # fp32 kernel and the trainer
+    # split-MFMA kernel's activation switch (sigmoid / softplus: the fp32
+    # kernel) and the trainer
     "relu": dict(D=4, C=0, K=16, layers=(128, 128), latent="normal", act="relu"),
     "gelu": dict(D=3, C=1, K=8, layers=(64, 64), latent="beta", act="gelu"),
     "tanh": dict(D=2, C=0, K=16, layers=(128,), latent="normal", act="tanh"),
@@ -45,18 +46,23 @@ CONFIGS = {
     "sigmoid": dict(D=2, C=2, K=16, layers=(64,), latent="beta", act="sigmoid"),
     "elu": dict(D=5, C=0, K=8, layers=(64, 64), latent="normal", act="elu"),
     "leaky_relu": dict(D=4, C=0, K=16, layers=(96,), latent="normal", act="leaky_relu"),
+    # one activation per coupling (a Chain of differently configured couplings)
+    "mixed": dict(D=4, C=0, K=16, layers=(128, 128), latent="normal", act=("relu", "swish", "gelu", "tanh")),
+    "mixed_fp32": dict(D=3, C=0, K=8, layers=(64,), latent="normal", act=("swish", "sigmoid", "elu")),
 }
-ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu"]
+ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu", "mixed", "mixed_fp32"]
 
 
 def chain_spec(cfg):
     D, K, layers = cfg["D"], cfg["K"], list(cfg["layers"])
     L = cfg.get("couplings", D)
+    acts = cfg.get("act", "swish")
+    acts = [acts] if isinstance(acts, str) else list(acts)  # a list: one per coupling, cycled
     bij = [{"type": "shift_bounds", "margin": cfg.get("margin", 0.1), "bounds": cfg.get("bounds", ())}]
-    for _ in range(L - 1):
-        bij.append({"type": "nsc", "knots": K, "layers": layers, "act": cfg.get("act", "swish")})
+    for i in range(L - 1):
+        bij.append({"type": "nsc", "knots": K, "layers": layers, "act": acts[i % len(acts)]})
         bij.append({"type": "roll", "shift": 1})
-    bij.append({"type": "nsc", "knots": K, "layers": layers, "act": cfg.get("act", "swish")})
+    bij.append({"type": "nsc", "knots": K, "layers": layers, "act": acts[(L - 1) % len(acts)]})
     return {"type": "chain", "bijectors": bij}
 
 

@@ -270,7 +270,7 @@ def test_golden_edges(name):
 # the fp32-MFMA kernel, which must stay parity-green on the same shapes.
 
 X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
-X3_ACTS = [a for a in ACTS if a not in ("sigmoid", "softplus")]
+X3_ACTS = [a for a in ACTS if a not in ("sigmoid", "softplus", "mixed_fp32")]
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"] + ACTS)

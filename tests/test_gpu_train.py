@@ -123,7 +123,7 @@ def _get(tree, path):
 
 GRAD_CASES = CASES + [("cfg1", 1024, 66), ("d8", 512, 67), ("d2h256", 256, 68), ("odd", 300, 69),
                       ("relu", 256, 70), ("gelu", 256, 71), ("tanh", 256, 72), ("softplus", 256, 73),
-                      ("sigmoid", 256, 74), ("elu", 256, 75), ("leaky_relu", 256, 76)]
+                      ("sigmoid", 256, 74), ("elu", 256, 75), ("leaky_relu", 256, 76), ("mixed", 256, 77)]
 
 
 @pytest.mark.parametrize("name,N,seed", GRAD_CASES)
