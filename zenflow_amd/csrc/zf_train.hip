@@ -475,7 +475,23 @@ int wgrad(int M, int N, int B, const Leaves& lv, const float* A, const float* G,
 template <class FX, class FY>
 __device__ __forceinline__ void leaf_sums2(FX x_at, FY y_at, int b0, int b1, double& s1, double& s2) {
   double a = 0.0, q = 0.0;
-  for (int b = b0; b < b1; ++b) {
+  int b = b0;
+  // eight rows' loads in flight before their (in-order) sums: the leaf is a
+  // chain of dependent adds, its loads are not
+  for (; b + 8 <= b1; b += 8) {
+    double xv[8], yv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xv[j] = (double)x_at(b + j);
+      yv[j] = (double)y_at(b + j);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a += xv[j];
+      q += xv[j] * yv[j];
+    }
+  }
+  for (; b < b1; ++b) {
     const double xv = (double)x_at(b), yv = (double)y_at(b);
     a += xv;
     q += xv * yv;
