@@ -688,12 +688,22 @@ constexpr int kMaxK = 64;
 // No per-thread arrays (they would live in scratch): the normalised widths and
 // heights are recomputed from p where needed, in the same float order.
 // gp may alias p (in-place reverse): every p[j] is read before gp[j] is written.
-template <bool GRAD>
-__device__ __forceinline__ void spline_one(const float* p, int K, float x, float& y, float& ld, float gy, float gl,
+// KT > 0: the knot count at compile time (8, 16, 32: every loop unrolled, so
+// the per-knot squareplus / divisions of different knots overlap instead of
+// running as one long dependent chain).  The same operations in the same
+// order as KT = 0 (the runtime-K form for other counts), but not always the
+// same bits: fp contraction may pair a multiply with a different add once
+// the loops are unrolled.  Every rank runs the same form, so the
+// data-parallel bit-identity holds.
+template <bool GRAD, int KT = 0>
+__device__ __forceinline__ void spline_one(const float* p, int Kr, float x, float& y, float& ld, float gy, float gl,
                                            float* gx, float* gp) {
+  constexpr int U = KT > 0 ? KT + 1 : 1;  // unroll counts (1: as written)
+  const int K = KT > 0 ? KT : Kr;
   const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // utils.py:32-34, Python floats
   const float cc = (float)c64, norm = (float)(1.0 + c64 * (double)K);
   float Sa = 0.f, Sb = 0.f;
+#pragma unroll U
   for (int j = 0; j < K; ++j) {
     Sa = Sa + sp_f(p[j]);
     Sb = Sb + sp_f(p[K + j]);
@@ -705,6 +715,7 @@ __device__ __forceinline__ void spline_one(const float* p, int K, float x, float
   int cnt = 0;
   {
     float tx = 0.f, ty = 0.f;
+#pragma unroll U
     for (int j = 0; j <= K; ++j) {
       if (tx <= x) {
         ++cnt;
@@ -728,6 +739,7 @@ __device__ __forceinline__ void spline_one(const float* p, int K, float x, float
     ld = oob ? 0.f : __builtin_nanf("");
     if (GRAD) {
       *gx = oob ? gy : __builtin_nanf("");
+#pragma unroll U
       for (int j = 0; j < 3 * K - 1; ++j) gp[j] = 0.f;
     }
     return;
@@ -775,18 +787,21 @@ __device__ __forceinline__ void spline_one(const float* p, int K, float x, float
   auto gw = [&](int j) { return j < idx ? g_xk : (j == idx ? g_wk : 0.f); };
   auto gh = [&](int j) { return j < idx ? g_yk : (j == idx ? g_hk : 0.f); };
   float tw = 0.f, th = 0.f;
+#pragma unroll U
   for (int j = 0; j < K; ++j) {
     tw += gw(j) * sp_f(p[j]);
     th += gh(j) * sp_f(p[K + j]);
   }
   const float gd0 = idx >= 1 ? g_dk * sp_grad(p[2 * K + idx - 1]) : 0.f;
   const float gd1 = idx + 1 < K ? g_dk1 * sp_grad(p[2 * K + idx]) : 0.f;
+#pragma unroll U
   for (int j = 0; j < K; ++j) {
     const float gsa = (gw(j) / Sa - tw / (Sa * Sa)) / norm;
     const float gsb = (gh(j) / Sb - th / (Sb * Sb)) / norm;
     gp[j] = gsa * sp_grad(p[j]);
     gp[K + j] = gsb * sp_grad(p[K + j]);
   }
+#pragma unroll U
   for (int j = 0; j < K - 1; ++j) gp[2 * K + j] = 0.f;
   if (idx >= 1) gp[2 * K + idx - 1] = 0.f + gd0;
   if (idx + 1 < K) gp[2 * K + idx] = 0.f + gd1;
@@ -799,6 +814,15 @@ __device__ __forceinline__ void spline_one(const float* p, int K, float x, float
 // column pmod(d + rot, D); thread d also carries the conditioning columns
 // dt + d, dt + d + dt, ... through unchanged.
 constexpr int kSplThreads = 64;
+
+// Launch LAUNCH(KT) with the compile-time knot count where instantiated.
+#define ZF_KNOT_DISPATCH(K, LAUNCH) \
+  do {                              \
+    if ((K) == 8) LAUNCH(8);        \
+    else if ((K) == 16) LAUNCH(16); \
+    else if ((K) == 32) LAUNCH(32); \
+    else LAUNCH(0);                 \
+  } while (0)
 
 // Global <-> LDS copies of n floats, 8 loads in flight per lane.
 __device__ __forceinline__ void stage_rows(float* sp, const float* __restrict__ src, long long n) {
@@ -828,6 +852,7 @@ __device__ __forceinline__ void unstage_rows(float* __restrict__ dst, const floa
 }
 
 // Forward: log-det summed per row in dim order through LDS.
+template <int KT>
 __global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __restrict__ s_in,
                                                                  float* __restrict__ s_out,
                                                                  const float* __restrict__ P, float* __restrict__ ld,
@@ -848,7 +873,7 @@ __global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __
     }
     const int col = pmodi(d + rot, D);
     float y, ldv;
-    spline_one<false>(sp + threadIdx.x * S, K, s_in[b * D + col], y, ldv, 0.f, 0.f, nullptr, nullptr);
+    spline_one<false, KT>(sp + threadIdx.x * S, K, s_in[b * D + col], y, ldv, 0.f, 0.f, nullptr, nullptr);
     s_out[b * D + col] = y;
     lds[threadIdx.x] = ldv;
   }
@@ -863,6 +888,7 @@ __global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __
 // Reverse: g_in = dL/d(state_in) from g_out = dL/d(state_out) and gl per row;
 // conditioning columns pass g_out through (their MLP share is added later).
 // dL/dP is formed in place in the staged rows and written back coalesced.
+template <int KT>
 __global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __restrict__ s_in,
                                                                  const float* __restrict__ P,
                                                                  const float* __restrict__ g_out, float gl,
@@ -884,7 +910,7 @@ __global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __
     const int col = pmodi(d + rot, D);
     float y, ldv, gx;
     float* row = sp + threadIdx.x * S;
-    spline_one<true>(row, K, s_in[b * D + col], y, ldv, g_out[b * D + col], gl, &gx, row);
+    spline_one<true, KT>(row, K, s_in[b * D + col], y, ldv, g_out[b * D + col], gl, &gx, row);
     g_in[b * D + col] = gx;
   }
   __syncthreads();
@@ -1449,9 +1475,11 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         }
       }
       const int rpb = zf::kSplThreads / dt;
-      hipLaunchKernelGGL(zf::spline_fwd_kernel, dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),
-                         (size_t)zf::kSplThreads * S * sizeof(float), st, sin, sout, nb.P,
-                         t->d_ld, B, D, dt, op.knots, rot);
+#define ZF_SPL(KTV) hipLaunchKernelGGL((zf::spline_fwd_kernel<KTV>), dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),\
+                         (size_t)zf::kSplThreads * S * sizeof(float), st, sin, sout, nb.P,\
+                         t->d_ld, B, D, dt, op.knots, rot)
+      ZF_KNOT_DISPATCH(op.knots, ZF_SPL);
+#undef ZF_SPL
       ZF_CHECK_LAUNCH("spline_fwd_kernel");
     } else {
       return zf::einval("op %d: unknown kind", i);
@@ -1490,9 +1518,11 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
     const int r = rots[i];
     // spline: g -> g_prev (transformed columns), gP
     const int rpb = zf::kSplThreads / dt;
-    hipLaunchKernelGGL(zf::spline_bwd_kernel, dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),
-                       (size_t)zf::kSplThreads * S * sizeof(float), st, state(i), nb.P, g, gl,
-                       g_prev, nb.gP, B, D, dt, op.knots, r);
+#define ZF_SPL(KTV) hipLaunchKernelGGL((zf::spline_bwd_kernel<KTV>), dim3(zf::blocks_for(B, rpb)), dim3(zf::kSplThreads),\
+                       (size_t)zf::kSplThreads * S * sizeof(float), st, state(i), nb.P, g, gl,\
+                       g_prev, nb.gP, B, D, dt, op.knots, r)
+    ZF_KNOT_DISPATCH(op.knots, ZF_SPL);
+#undef ZF_SPL
     ZF_CHECK_LAUNCH("spline_bwd_kernel");
     // MLP reverse
     const float* gout = nb.gP;
