@@ -46,6 +46,9 @@ int zf_device_synchronize(void);
 int zf_malloc(void** ptr, size_t bytes);
 int zf_free(void* ptr);
 int zf_memset_async(void* ptr, int value, size_t bytes, void* stream);
+/* Host <-> device copies, ordered on `stream`.  htod returns once `src` may be
+ * reused (the copy itself completes in stream order); dtoh returns with `dst`
+ * filled (up to 4 MiB through a pinned staging buffer). */
 int zf_memcpy_htod(void* dst, const void* src, size_t bytes, void* stream);
 int zf_memcpy_dtoh(void* dst, const void* src, size_t bytes, void* stream);
 int zf_memcpy_dtod(void* dst, const void* src, size_t bytes, void* stream);
