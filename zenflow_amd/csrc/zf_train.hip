@@ -75,7 +75,8 @@ __device__ __forceinline__ void gemm_epilogue(float v, int n, long long o, float
 
 // SPLITQ: block z = q of a 64 x 64 tile multiplies only the k-pairs
 // p = q (mod 4) — exactly accumulator set q of the NACC = 4 kernel, in the
-// same order — into part[q][M][N]; gemm_combine_kernel then forms
+// same order (trailing all-zero pairs aside, which only turn -0 into +0) —
+// into part[q][M][N]; gemm_combine_kernel then forms
 // (P0 + P1) + (P2 + P3) and the epilogue: the same bits from four times the
 // blocks (small batches: 1024 rows give 32 tiles for 256 CUs).
 template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
@@ -93,22 +94,30 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int kbeg = WG ? blockIdx.z * KC : 0;
-  const int kend = WG ? min(K, kbeg + KC) : K;
+  // SPLITQ: block q runs a virtual k range holding only its k-pairs
+  // p = q, q + 4, q + 8, ... (virtual pair v = real pair 4 v + q), so one
+  // k-tile of loads serves 16 of its pairs instead of 4
+  const int q4 = SPLITQ ? (int)blockIdx.z : 0;
+  const int kend = WG ? min(K, kbeg + KC) : SPLITQ ? 2 * max(0, ((K + 1) / 2 - q4 + 3) / 4) : K;
+  auto real_k = [&](int k) { return SPLITQ ? 2 * (4 * (k >> 1) + q4) + (k & 1) : k; };
+  const int kmax = SPLITQ ? K : kend;
   float ra[NA], rb[NB];
   auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int e = tid + 256 * i;
       const int mm = TA ? (e % BM) : (e / MBK), kk = TA ? (e / BM) : (e % MBK);
-      const int m = m0 + mm, k = k0 + kk;
-      ra[i] = (m < M && k < kend) ? (TA ? A[(long long)k * lda + m] : A[(long long)m * lda + k]) : 0.f;
+      const int m = m0 + mm, k = real_k(k0 + kk);
+      ra[i] = (m < M && k0 + kk < kend && k < kmax) ? (TA ? A[(long long)k * lda + m] : A[(long long)m * lda + k])
+                                                    : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int e = tid + 256 * i;
       const int nn = TB ? (e / MBK) : (e % BN), kk = TB ? (e % MBK) : (e / BN);
-      const int n = n0 + nn, k = k0 + kk;
-      rb[i] = (n < N && k < kend) ? (TB ? B[(long long)n * ldb + k] : B[(long long)k * ldb + n]) : 0.f;
+      const int n = n0 + nn, k = real_k(k0 + kk);
+      rb[i] = (n < N && k0 + kk < kend && k < kmax) ? (TB ? B[(long long)n * ldb + k] : B[(long long)k * ldb + n])
+                                                    : 0.f;
     }
   };
   auto store = [&]() {
@@ -146,10 +155,8 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
     store();
     __syncthreads();
     if (k0 + MBK < kend) load(k0 + MBK);
-    const int kq = SPLITQ ? 2 * (int)blockIdx.z : 0;
 #pragma unroll
-    for (int kb0 = 0; kb0 < MBK; kb0 += SPLITQ ? 8 : 2) {
-      const int kb = kb0 + kq;
+    for (int kb = 0; kb < MBK; kb += 2) {
       float a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) a[i] = As[kb + h][wm0 + 32 * i + r];
