@@ -321,6 +321,8 @@ inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t 
 
 // Split-K workspace (floats) shared by the batch reductions below.
 constexpr int64_t kWsFloats = 32ll << 20;
+// The split-set GEMMs' partials (4 M N floats, M N < 256 tiles of 64 x 64).
+constexpr int64_t kSplitFloats = 4ll << 20;
 
 // ---- batch reductions: row leaves + one fixed pairwise tree ----------------
 // Every sum over the batch rows (weight and bias gradients, BatchNorm sums
@@ -474,6 +476,95 @@ int wgrad(int M, int N, int B, const Leaves& lv, const float* A, const float* G,
 #undef ZF_L
   }
   ZF_CHECK_LAUNCH("wgrad_tree");
+  return ZF_OK;
+}
+
+// Weight-gradient trees of several layers in one launch: the backward pass
+// writes each layer's leaf partials to its own slice of the split-K
+// workspace and the trees of all of them run at the end (or when the
+// workspace or the item list is full) — one launch instead of one per layer,
+// the same per-element trees (wgrad_tree's), so the same bits.
+constexpr int kTreeItems = 24;
+struct TreeItem {
+  const float* part;
+  double* dW;
+  double* db;
+  int M, N, n, blocks;  // blocks of 64 elements
+};
+struct TreeBatch {
+  int count;
+  TreeItem it[kTreeItems];
+};
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void wgrad_tree_batch(TreeBatch tb) {
+  __shared__ double r[4][64];
+  int b = blockIdx.x, i = 0;
+  while (i + 1 < tb.count && b >= tb.it[i].blocks) b -= tb.it[i++].blocks;
+  const TreeItem& t = tb.it[i];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int P = t.n < 4 ? t.n : 4, m = t.n / P;
+  const long long idx = (long long)b * 64 + lane;
+  const long long MN1 = (long long)(t.M + 1) * t.N;
+  if (w < P && idx < MN1) r[w][lane] = tree_n<NMAX>(t.part + (long long)w * m * MN1 + idx, MN1, m);
+  __syncthreads();
+  if (w != 0 || idx >= MN1) return;
+  double v = r[0][lane];
+  if (P == 2) v = v + r[1][lane];
+  else if (P == 4) v = (v + r[1][lane]) + (r[2][lane] + r[3][lane]);
+  if (idx < (long long)t.M * t.N) t.dW[idx] = v;
+  else t.db[idx - (long long)t.M * t.N] = v;
+}
+
+struct WgradQueue {
+  TreeBatch tb;
+  int64_t used = 0;  // workspace floats holding pending partials
+  int nmax = 1;
+};
+
+int wgrad_flush(WgradQueue& q, hipStream_t st) {
+  if (q.tb.count == 0) return ZF_OK;
+  int blocks = 0;
+  for (int i = 0; i < q.tb.count; ++i) blocks += q.tb.it[i].blocks;
+  const int nm = q.nmax < 4 ? 1 : q.nmax / 4;
+#define ZF_L(NM) hipLaunchKernelGGL((wgrad_tree_batch<NM>), dim3(blocks), dim3(256), 0, st, q.tb)
+  ZF_NMAX_DISPATCH(nm, ZF_L);
+#undef ZF_L
+  ZF_CHECK_LAUNCH("wgrad_tree_batch");
+  q.tb.count = 0;
+  q.used = 0;
+  q.nmax = 1;
+  return ZF_OK;
+}
+
+// wgrad with the tree deferred into `q` (one level of leaves: n <= 64);
+// more leaves run wgrad's two-level form at once, after the queue.
+int wgrad_deferred(WgradQueue& q, int M, int N, int B, const Leaves& lv, const float* A, const float* G, double* dW,
+                   double* db, float* ws, double* ws2, hipStream_t st) {
+  const int64_t MN1 = (int64_t)(M + 1) * N, need = (int64_t)lv.n * MN1;
+  int rc;
+  if (lv.n > kMaxLeaves) {
+    if ((rc = wgrad_flush(q, st))) return rc;
+    return wgrad(M, N, B, lv, A, G, dW, db, ws, ws2, st);
+  }
+  if (need > kWsFloats) return enotsup("training: weight-gradient workspace");
+  if (q.used + need > kWsFloats || q.tb.count == kTreeItems)
+    if ((rc = wgrad_flush(q, st))) return rc;
+  float* part = ws + q.used;
+  hipLaunchKernelGGL((mgemm_kernel<64, 64, true, false, true>), dim3((N + 63) / 64, (M + 63) / 64, lv.n), dim3(256), 0,
+                     st, M, N, B, A, M, G, N, part, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows,
+                     (int)ZF_ACT_SWISH);
+  ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
+  TreeItem& it = q.tb.it[q.tb.count++];
+  it.part = part;
+  it.dW = dW;
+  it.db = db;
+  it.M = M;
+  it.N = N;
+  it.n = lv.n;
+  it.blocks = (int)blocks_for(MN1, 64);
+  q.used += need;
+  q.nmax = std::max(q.nmax, lv.n);
   return ZF_OK;
 }
 
@@ -1182,6 +1273,7 @@ struct zf_trainer {
   int64_t gath_bytes = 0;
   void* d_colws = nullptr;
   float* d_ws = nullptr;      // split-K partials (kWsFloats)
+  float* d_split = nullptr;   // split-set GEMM partials (kSplitFloats)
   int64_t colws_bytes = 0;
   struct NscBufs {
     float *U, *Uhat, *Ubn, *P, *gP, *gU, *gA, *gB;
@@ -1273,6 +1365,7 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_rowloss = (double*)zf::dmalloc(t, 2 * B, rc);
   t->d_g64 = (double*)zf::dmalloc(t, 2 * need, rc);
   t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
+  t->d_split = zf::dmalloc(t, zf::kSplitFloats, rc);
   t->d_c = zf::dmalloc(t, B * (desc.cond_dim > 0 ? desc.cond_dim : 1), rc);
   t->d_bc = zf::dmalloc(t, 4, rc);
   {
@@ -1473,8 +1566,8 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
         const int out_w = last ? dt * S : op.hidden[l];
         float* Z = last ? nb.P : nb.Z[l];
         rc = zf::gemm(false, Bg, B, out_w, in_w, in, in_w, nat + op.off_w[l], out_w, Z, out_w, st, zf::kEpiBias,
-                      nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act, t->splitq ? t->d_ws : nullptr,
-                      zf::kWsFloats);
+                      nat + op.off_b[l], last ? nullptr : nb.H[l], nullptr, op.act, t->splitq ? t->d_split : nullptr,
+                      zf::kSplitFloats);
         if (rc) return rc;
         if (!last) {
           in = nb.H[l];
@@ -1516,6 +1609,8 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
   // ---- reverse ----
   ZF_TRY_HIP(hipMemsetAsync(G64, 0, (size_t)t->nat_floats * sizeof(double), st));
   const float gl = -1.0f / (float)Bg;  // d loss / d log_det of every op and row
+  zf::WgradQueue wq;
+  wq.tb.count = 0;
   for (int i = desc.n_ops - 1; i >= 0; --i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind == ZF_OP_ROLL || op.kind == ZF_OP_SHIFT_BOUNDS) continue;  // Roll: index map; SB: first op
@@ -1542,15 +1637,15 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       // dW_l = hin^T . gout ; db_l = colsum(gout): leaves capped by the
       // split-K workspace (a power of two, the same on every rank)
       const int cap = pow2floor(std::min<int64_t>(kLeafCap, std::max<int64_t>(1, kWsFloats / ((int64_t)(in_w + 1) * out_w))));
-      rc = zf::wgrad(in_w, out_w, B, leaves_for(B, Bg, W, cap), hin, gout, G64 + op.off_w[l], G64 + op.off_b[l],
-                     t->d_ws, t->d_ws2, st);
+      rc = zf::wgrad_deferred(wq, in_w, out_w, B, leaves_for(B, Bg, W, cap), hin, gout, G64 + op.off_w[l],
+                              G64 + op.off_b[l], t->d_ws, t->d_ws2, st);
       if (rc) return rc;
       // g_in = gout . W_l^T
       float* gin = l == 0 ? nb.gU : gbufs[which];
       // (through swish of layer l-1 when l > 0)
       rc = zf::gemm(true, Bg, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
                     l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act,
-                    t->splitq ? t->d_ws : nullptr, zf::kWsFloats);
+                    t->splitq ? t->d_split : nullptr, zf::kSplitFloats);
       if (rc) return rc;
       if (l > 0) {
         gout = gin;
@@ -1587,6 +1682,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
     g = g_prev;
     g_prev = tmp;
   }
+  if ((rc = zf::wgrad_flush(wq, st))) return rc;
   // ---- the gradient: (all ranks' fp64 shares, tree over ranks) -> fp32 ----
   if (W > 1) {
     rc = t->comm.allgather(t->comm.ctx, G64, t->d_gath, (size_t)t->nat_floats * sizeof(double), st);
