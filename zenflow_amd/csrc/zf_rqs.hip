@@ -117,12 +117,17 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
 
 // Direct (no-LDS) path for K % 4 == 0: one thread per (row, dim) item reads
 // its own dx/dy rows as K/4 dwordx4 each (a 64-B row per array at K=16; the
-// thread consumes every byte it fetches), keeps the knots in registers and
-// gathers only the two slopes its bin needs.  Nothing is staged, no barrier
+// thread consumes every byte it fetches) and keeps the knots in registers.
+// Slopes (SM): 0 = gather only the two the bin needs, after the search;
+// 1 = load the whole slope row with the knots and pick the two in the search
+// sweep (no dependent second memory round trip).  Measured (bench_rqs, same
+// box): SM 1 +5% at K = 16 (forward 0.667 -> 0.70 of HBM, inverse 0.69 ->
+// 0.715), -12% at K = 32 (register pressure), even at K = 8; the aligned-
+// float4 window form of SM 1 lost at every K.  Nothing is staged, no barrier
 // sits between a wave's loads and its math, so every wave streams
 // independently.  The row log-det (sum over N dims, dim order) goes through
 // a tiny LDS array.
-template <bool FWD, int K>
+template <bool FWD, int K, int SM>
 __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
     const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
     const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
@@ -147,7 +152,15 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
   }
   const float v = xin[item];
   const float* slp = slope + item * (K - 1);
-  const RqsBin bn = rqs_bin_regs<FWD, K>(v, w, h, [&](int j) { return slp[j]; });
+  RqsBin bn;
+  if constexpr (SM == 0) {
+    bn = rqs_bin_regs<FWD, K>(v, w, h, [&](int j) { return slp[j]; });
+  } else {
+    float sl[K - 1];
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) sl[j] = slp[j];
+    bn = rqs_bin_regs_sl<FWD, K>(v, w, h, sl, [](float s) { return s; });
+  }
   if (FWD) {
     float y, l;
     rqs_forward_eval(v, bn, y, l);
@@ -357,9 +370,9 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
     const int R = kK1Threads / N;
     const int64_t grid = (M + R - 1) / R;
     if (grid > 0x7fffffffLL) return einval("M too large");
-#define ZF_RQSD(KV)                                                                                  \
-  hipLaunchKernelGGL((rqs_kernel_direct<FWD, KV>), dim3((unsigned)grid), dim3(kK1Threads), 0, st, x, \
-                     dx, dy, slope, out, log_det, M, N, R)
+#define ZF_RQSD(KV)                                                                                   \
+  hipLaunchKernelGGL((rqs_kernel_direct<FWD, KV, KV == 16>), dim3((unsigned)grid), dim3(kK1Threads), 0, \
+                     st, x, dx, dy, slope, out, log_det, M, N, R)
     switch (K) {
       case 4: ZF_RQSD(4); break;
       case 8: ZF_RQSD(8); break;
