@@ -775,8 +775,31 @@ __global__ void bn_apply_kernel(const float* __restrict__ U, const float* __rest
   Ubn[i] = bn_out(uh, scale[k], bias[k]);
 }
 
-__device__ __forceinline__ float sp_f(float x) { return 0.5f * (x + sqrtf(x * x + 4.0f)); }
-__device__ __forceinline__ float sp_grad(float x) { return 0.5f * (1.0f + x / sqrtf(x * x + 4.0f)); }
+// Spline-path arithmetic at a third of the IEEE expansions' instructions (the
+// per-thread spline kernels are issue-latency bound: one wave per (row block),
+// thousands of dependent VALU): a hardware reciprocal / square root with one
+// Newton or residual step, and quotients by a loop-invariant divisor as one
+// residual correction of x * rcp(d) — the correctly rounded result for these
+// normal operands, as zf_flow_dev.h's div_cr in the inference kernels.
+__device__ __forceinline__ float t_rcp(float x) {
+  const float r = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float t_div(float x, float d, float r) {
+  const float q = x * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
+}
+// sqrt(x^2 + 4) (>= 2: never denormal), residual-corrected hardware root
+__device__ __forceinline__ float t_sq4(float x) {
+  const float a = x * x + 4.0f;
+  const float sq = __builtin_amdgcn_sqrtf(a);
+  return __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * __builtin_amdgcn_rcpf(sq), sq);
+}
+__device__ __forceinline__ float sp_f(float x) { return 0.5f * (x + t_sq4(x)); }
+__device__ __forceinline__ float sp_grad(float x) {
+  const float sq = t_sq4(x);
+  return 0.5f * (1.0f + t_div(x, sq, t_rcp(sq)));
+}
 
 constexpr int kMaxK = 64;
 
@@ -811,6 +834,7 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
   // are the bin's left edge (xk, yk)
   float xk = 0.f, yk = 0.f;
   int cnt = 0;
+  const float rSa = t_rcp(Sa), rSb = t_rcp(Sb), rnorm = t_rcp(norm);
   {
     float tx = 0.f, ty = 0.f;
 #pragma unroll U
@@ -821,8 +845,8 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
         yk = ty;
       }
       if (j < K) {
-        tx = tx + (sp_f(p[j]) / Sa + cc) / norm;
-        ty = ty + (sp_f(p[K + j]) / Sb + cc) / norm;
+        tx = tx + t_div(t_div(sp_f(p[j]), Sa, rSa) + cc, norm, rnorm);
+        ty = ty + t_div(t_div(sp_f(p[K + j]), Sb, rSb) + cc, norm, rnorm);
       }
     }
   }
@@ -842,7 +866,8 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
     }
     return;
   }
-  const float wk = (sp_f(p[idx]) / Sa + cc) / norm, hk = (sp_f(p[K + idx]) / Sb + cc) / norm;
+  const float wk = t_div(t_div(sp_f(p[idx]), Sa, rSa) + cc, norm, rnorm);
+  const float hk = t_div(t_div(sp_f(p[K + idx]), Sb, rSb) + cc, norm, rnorm);
   const float dk = (idx == 0) ? 1.f : sp_f(p[2 * K + idx - 1]);
   const float dk1 = (idx + 1 == K) ? 1.f : sp_f(p[2 * K + idx]);
   const float sk = hk / wk;
@@ -892,10 +917,11 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
   }
   const float gd0 = idx >= 1 ? g_dk * sp_grad(p[2 * K + idx - 1]) : 0.f;
   const float gd1 = idx + 1 < K ? g_dk1 * sp_grad(p[2 * K + idx]) : 0.f;
+  const float twq = tw / (Sa * Sa), thq = th / (Sb * Sb);
 #pragma unroll U
   for (int j = 0; j < K; ++j) {
-    const float gsa = (gw(j) / Sa - tw / (Sa * Sa)) / norm;
-    const float gsb = (gh(j) / Sb - th / (Sb * Sb)) / norm;
+    const float gsa = t_div(t_div(gw(j), Sa, rSa) - twq, norm, rnorm);
+    const float gsb = t_div(t_div(gh(j), Sb, rSb) - thq, norm, rnorm);
     gp[j] = gsa * sp_grad(p[j]);
     gp[K + j] = gsb * sp_grad(p[K + j]);
   }
