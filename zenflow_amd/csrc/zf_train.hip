@@ -948,17 +948,21 @@ constexpr int kSplThreads = 64;
     else LAUNCH(0);                 \
   } while (0)
 
-// Global <-> LDS copies of n floats, 8 loads in flight per lane.
+// Global <-> LDS copies of n floats, kStageInflight loads in flight per lane
+// (the per-thread spline kernels run one wave per block: every serial HBM
+// round trip here is exposed — 24 in flight stage K = 16's 47 floats per
+// lane in two rounds instead of six).
+constexpr int kStageInflight = 24;
 __device__ __forceinline__ void stage_rows(float* sp, const float* __restrict__ src, long long n) {
-  for (long long e0 = threadIdx.x; e0 < n; e0 += 8 * kSplThreads) {
-    float v[8];
+  for (long long e0 = threadIdx.x; e0 < n; e0 += kStageInflight * kSplThreads) {
+    float v[kStageInflight];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kStageInflight; ++u) {
       const long long e = e0 + u * kSplThreads;
       v[u] = e < n ? src[e] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kStageInflight; ++u) {
       const long long e = e0 + u * kSplThreads;
       if (e < n) sp[e] = v[u];
     }
@@ -987,17 +991,18 @@ __global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __
   const int lr = threadIdx.x / dt, d = threadIdx.x - lr * dt;
   const long long b0 = (long long)blockIdx.x * rpb, b = b0 + lr;
   const int nrows = (int)(B - b0 < rpb ? B - b0 : rpb);
+  const bool ok = lr < nrows;
+  const int col = pmodi(d + rot, D);
+  const float xv = ok ? s_in[b * D + col] : 0.f;  // in flight with the staging loads
   stage_rows(sp, P + b0 * dt * S, (long long)nrows * dt * S);
   __syncthreads();
-  const bool ok = lr < nrows;
   if (ok) {
     for (int j = dt + d; j < D; j += dt) {
       const int cj = pmodi(j + rot, D);
       s_out[b * D + cj] = s_in[b * D + cj];
     }
-    const int col = pmodi(d + rot, D);
     float y, ldv;
-    spline_one<false, KT>(sp + threadIdx.x * S, K, s_in[b * D + col], y, ldv, 0.f, 0.f, nullptr, nullptr);
+    spline_one<false, KT>(sp + threadIdx.x * S, K, xv, y, ldv, 0.f, 0.f, nullptr, nullptr);
     s_out[b * D + col] = y;
     lds[threadIdx.x] = ldv;
   }
@@ -1024,17 +1029,19 @@ __global__ __launch_bounds__(kSplThreads) void spline_bwd_kernel(const float* __
   const long long b0 = (long long)blockIdx.x * rpb, b = b0 + lr;
   const int nrows = (int)(B - b0 < rpb ? B - b0 : rpb);
   const long long n = (long long)nrows * dt * S;
+  const bool ok = lr < nrows;
+  const int col = pmodi(d + rot, D);
+  const float xv = ok ? s_in[b * D + col] : 0.f, gv = ok ? g_out[b * D + col] : 0.f;  // in flight with the staging
   stage_rows(sp, P + b0 * dt * S, n);
   __syncthreads();
-  if (lr < nrows) {
+  if (ok) {
     for (int j = dt + d; j < D; j += dt) {
       const int cj = pmodi(j + rot, D);
       g_in[b * D + cj] = g_out[b * D + cj];
     }
-    const int col = pmodi(d + rot, D);
     float y, ldv, gx;
     float* row = sp + threadIdx.x * S;
-    spline_one<true, KT>(row, K, s_in[b * D + col], y, ldv, g_out[b * D + col], gl, &gx, row);
+    spline_one<true, KT>(row, K, xv, y, ldv, gv, gl, &gx, row);
     g_in[b * D + col] = gx;
   }
   __syncthreads();
