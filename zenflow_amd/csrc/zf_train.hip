@@ -570,23 +570,27 @@ int wgrad_deferred(WgradQueue& q, int M, int N, int B, const Leaves& lv, const f
 
 // Leaf sums of two per-column sums over rows [b0, b1), in row order, fp64:
 // s1 = sum x, s2 = sum x * y (y = x: the sum of squares).
+constexpr int kLeafInflight = 32;
 template <class FX, class FY>
 __device__ __forceinline__ void leaf_sums2(FX x_at, FY y_at, int b0, int b1, double& s1, double& s2) {
   double a = 0.0, q = 0.0;
   int b = b0;
-  // eight rows' loads in flight before their (in-order) sums: the leaf is a
-  // chain of dependent adds, its loads are not
-  for (; b + 8 <= b1; b += 8) {
-    double xv[8], yv[8];
+  // kLeafInflight rows' loads in flight before their (in-order) sums: the
+  // leaf is a chain of dependent adds, its loads are not (the one-block
+  // BatchNorm kernels expose every serial round trip: 32 rows, a whole leaf
+  // at the default batch, in one)
+  constexpr int R = kLeafInflight;
+  for (; b + R <= b1; b += R) {
+    float xv[R], yv[R];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      xv[j] = (double)x_at(b + j);
-      yv[j] = (double)y_at(b + j);
+    for (int j = 0; j < R; ++j) {
+      xv[j] = x_at(b + j);
+      yv[j] = y_at(b + j);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a += xv[j];
-      q += xv[j] * yv[j];
+    for (int j = 0; j < R; ++j) {
+      a += (double)xv[j];
+      q += (double)xv[j] * (double)yv[j];
     }
   }
   for (; b < b1; ++b) {
@@ -950,9 +954,9 @@ constexpr int kSplThreads = 64;
 
 // Global <-> LDS copies of n floats, kStageInflight loads in flight per lane
 // (the per-thread spline kernels run one wave per block: every serial HBM
-// round trip here is exposed — 24 in flight stage K = 16's 47 floats per
-// lane in two rounds instead of six).
-constexpr int kStageInflight = 24;
+// round trip here is exposed — 48 in flight stage K = 16's 47 floats per
+// lane in one round instead of six).
+constexpr int kStageInflight = 48;
 __device__ __forceinline__ void stage_rows(float* sp, const float* __restrict__ src, long long n) {
   for (long long e0 = threadIdx.x; e0 < n; e0 += kStageInflight * kSplThreads) {
     float v[kStageInflight];
