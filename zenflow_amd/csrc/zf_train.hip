@@ -874,23 +874,25 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
   const float hk = t_div(t_div(sp_f(p[K + idx]), Sb, rSb) + cc, norm, rnorm);
   const float dk = (idx == 0) ? 1.f : sp_f(p[2 * K + idx - 1]);
   const float dk1 = (idx + 1 == K) ? 1.f : sp_f(p[2 * K + idx]);
-  const float sk = hk / wk;
-  const float zr = (x - xk) / wk;
+  const float rwk = t_rcp(wk);
+  const float sk = t_div(hk, wk, rwk);
+  const float zr = t_div(x - xk, wk, rwk);
   const float z = fminf(fmaxf(zr, kEpsT), 0.99999f);
   const float az = 1.0f - z;
   const float num = hk * z * (sk * z + dk * az);
   const float den = sk + (dk1 + dk - 2.0f * sk) * z * az;
-  y = yk + num / (den + kEpsT);
+  const float dE = den + kEpsT, rdE = t_rcp(dE);
+  y = yk + t_div(num, dE, rdE);
   const float q = z * (dk1 * z + 2.0f * sk * az) + dk * (az * az);
   ld = 2.0f * logf(sk + kEpsT) + logf(q + kEpsT) - 2.0f * logf(den + kEpsT);
   if (!GRAD) return;
   // ---- reverse pass ----
-  const float dE = den + kEpsT;
   float g_yk = gy;
-  const float g_num = gy / dE;
-  float g_den = -gy * num / (dE * dE) - 2.0f * gl / dE;
-  float g_sk = 2.0f * gl / (sk + kEpsT);
-  const float g_q = gl / (q + kEpsT);
+  const float g_num = t_div(gy, dE, rdE);
+  const float dE2 = dE * dE, skE = sk + kEpsT, qE = q + kEpsT;
+  float g_den = t_div(-gy * num, dE2, t_rcp(dE2)) - t_div(2.0f * gl, dE, rdE);
+  float g_sk = t_div(2.0f * gl, skE, t_rcp(skE));
+  const float g_q = t_div(gl, qE, t_rcp(qE));
   float g_hk = g_num * (sk * z * z + dk * z * az);
   g_sk += g_num * hk * z * z;
   float g_dk = g_num * hk * z * az;
@@ -904,11 +906,12 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
   g_dk += g_q * az * az;
   g_z += g_q * (2.0f * dk1 * z + 2.0f * sk * (az - z) - 2.0f * dk * az);
   const float g_zr = (zr > kEpsT && zr < 0.99999f) ? g_z : 0.f;  // jnp.clip passes inside only
-  *gx = g_zr / wk;
-  const float g_xk = -g_zr / wk;
-  float g_wk = -g_zr * zr / wk;
-  g_hk += g_sk / wk;
-  g_wk += -g_sk * hk / (wk * wk);
+  *gx = t_div(g_zr, wk, rwk);
+  const float g_xk = t_div(-g_zr, wk, rwk);
+  float g_wk = t_div(-g_zr * zr, wk, rwk);
+  g_hk += t_div(g_sk, wk, rwk);
+  const float wk2 = wk * wk;
+  g_wk += t_div(-g_sk * hk, wk2, t_rcp(wk2));
   // gradient w.r.t. widths / heights: xk = sum_{j<idx} w_j (likewise yk), plus
   // the bin's own w_idx, h_idx; then through w_j = (sa_j / Sa + c) / norm
   auto gw = [&](int j) { return j < idx ? g_xk : (j == idx ? g_wk : 0.f); };
@@ -921,7 +924,8 @@ __device__ __forceinline__ void spline_one(const float* p, int Kr, float x, floa
   }
   const float gd0 = idx >= 1 ? g_dk * sp_grad(p[2 * K + idx - 1]) : 0.f;
   const float gd1 = idx + 1 < K ? g_dk1 * sp_grad(p[2 * K + idx]) : 0.f;
-  const float twq = tw / (Sa * Sa), thq = th / (Sb * Sb);
+  const float Sa2 = Sa * Sa, Sb2 = Sb * Sb;
+  const float twq = t_div(tw, Sa2, t_rcp(Sa2)), thq = t_div(th, Sb2, t_rcp(Sb2));
 #pragma unroll U
   for (int j = 0; j < K; ++j) {
     const float gsa = t_div(t_div(gw(j), Sa, rSa) - twq, norm, rnorm);
