@@ -7,9 +7,9 @@
 // K % 4 == 0 (4/8/16/32, 16-B aligned params): rqs_kernel_direct, one thread
 // per item streaming its own dx/dy rows as dwordx4 straight to registers
 // (no LDS staging or barrier between a wave's loads and its math: measured
-// 2x the LDS-staged variant, 5.3-5.6 TB/s at K=16).  Other K: rqs_kernel,
+// 2x the LDS-staged variant; 5.7-5.8 TB/s at K=16).  Other K: rqs_kernel,
 // rows staged through LDS with an odd stride.  The row log-det is summed in
-// dim order (utils.py:139) through LDS.
+// dim order (utils.py:139), by lane shuffles where a row's items share a wave.
 #include "zf_internal.h"
 #include "zf_spline.h"
 
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
 // 0.715), -12% at K = 32 (register pressure), even at K = 8; the aligned-
 // float4 window form of SM 1 lost at every K.  Nothing is staged, no barrier
 // sits between a wave's loads and its math, so every wave streams
-// independently.  The row log-det (sum over N dims, dim order) goes through
-// a tiny LDS array.
+// independently.  The row log-det (sum over N dims, dim order) goes by lane
+// shuffles (N a power of two) or through a tiny LDS array.
 template <bool FWD, int K, int SM>
 __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
     const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
