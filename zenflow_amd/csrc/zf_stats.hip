@@ -46,26 +46,53 @@ __global__ __launch_bounds__(kStatThreads) void colstats_partial(
     if (r1 > N) r1 = N;
     const int mode = pre.mode[col];
     const float a = pre.a[col];
-    for (long long r = r0 + sub; r < r1; r += lanes_per_col) {
-      const float v = pre_transform(x[r * ld + col_offset + col], mode, a);
+    auto acc = [&](float raw) {
+      const float v = pre_transform(raw, mode, a);
       // jnp.min/max propagate NaN
       if (v != v) { mn = v; mx = v; }
       else if (mn == mn) { mn = fminf(mn, v); mx = fmaxf(mx, v); }
       sm += (double)v;
       sq += (double)v * (double)v;
+    };
+    // kU rows' loads in flight ahead of the in-order accumulation (a small
+    // batch is one block: every serial round trip would be exposed)
+    constexpr int kU = 8;
+    long long r = r0 + sub;
+    for (; r + (kU - 1) * (long long)lanes_per_col < r1; r += kU * (long long)lanes_per_col) {
+      float vv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) vv[u] = x[(r + u * (long long)lanes_per_col) * ld + col_offset + col];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc(vv[u]);
     }
+    for (; r < r1; r += lanes_per_col) acc(x[r * ld + col_offset + col]);
   }
   smin[t] = mn; smax[t] = mx; ssum[t] = sm; ssq[t] = sq;
   __syncthreads();
   if (t < ncols) {
     float m0 = INFINITY, m1 = -INFINITY;
     double a0 = 0.0, a1 = 0.0;
-    for (int k = 0; k < lanes_per_col; ++k) {
+    auto comb = [&](float lo, float hi, double s1, double s2) {
+      if (lo != lo || m0 != m0) { m0 = m0 != m0 ? m0 : lo; m1 = m0; }
+      else { m0 = fminf(m0, lo); m1 = fmaxf(m1, hi); }
+      a0 += s1;
+      a1 += s2;
+    };
+    int k = 0;
+    for (; k + 8 <= lanes_per_col; k += 8) {  // eight entries' LDS reads ahead of the in-order combine
+      float lo[8], hi[8];
+      double s1[8], s2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = (k + u) * ncols + t;
+        lo[u] = smin[i]; hi[u] = smax[i]; s1[u] = ssum[i]; s2[u] = ssq[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) comb(lo[u], hi[u], s1[u], s2[u]);
+    }
+    for (; k < lanes_per_col; ++k) {
       const int i = k * ncols + t;
-      if (smin[i] != smin[i] || m0 != m0) { m0 = m0 != m0 ? m0 : smin[i]; m1 = m0; }
-      else { m0 = fminf(m0, smin[i]); m1 = fmaxf(m1, smax[i]); }
-      a0 += ssum[i];
-      a1 += ssq[i];
+      comb(smin[i], smax[i], ssum[i], ssq[i]);
     }
     const size_t o = (size_t)blockIdx.x * ncols + t;
     pmin[o] = m0; pmax[o] = m1; psum[o] = a0; psq[o] = a1;
