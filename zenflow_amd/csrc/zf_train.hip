@@ -390,6 +390,22 @@ __device__ __forceinline__ void lds_tree(double* p, int n, int ncols, int stride
   }
 }
 
+// Two such trees (same shapes) level by level under one barrier per level:
+// each tree's pairwise sums are unchanged.
+__device__ __forceinline__ void lds_tree2(double* p, double* q, int n, int ncols, int stride) {
+  for (int s = 1; s < n; s *= 2) {
+    const int pairs = (n + 2 * s - 1) / (2 * s);
+    for (int t = threadIdx.x; t < pairs * ncols; t += blockDim.x) {
+      const int j = t / ncols, k = t - j * ncols, i = 2 * s * j;
+      if (i + s < n) {
+        p[i * stride + k] = p[i * stride + k] + p[(i + s) * stride + k];
+        q[i * stride + k] = q[i * stride + k] + q[(i + s) * stride + k];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Launch KERNEL<..., NMAX> with the smallest register tree that holds n leaves.
 #define ZF_NMAX_DISPATCH(n, LAUNCH) \
   do {                              \
@@ -1093,8 +1109,7 @@ __global__ __launch_bounds__(1024) void bn_fwd_small(const float* __restrict__ s
     leaf_sums2([&](int b) { return u_at(b, k); }, [&](int b) { return u_at(b, k); }, b0, b1, p1[t], p2[t]);
   }
   __syncthreads();
-  lds_tree(p1, n, DC, DC);
-  lds_tree(p2, n, DC, DC);
+  lds_tree2(p1, p2, n, DC, DC);
   if (tid < DC) {
     float mean, rstd;
     bn_stats_one(p1[tid], p2[tid], B, tid, DC, nat_bn, mean, rstd, update);
@@ -1132,8 +1147,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_small(const float* __restrict__ g
                b0, b1, p1[t], p2[t]);
   }
   __syncthreads();
-  lds_tree(p1, n, DC, DC);
-  lds_tree(p2, n, DC, DC);
+  lds_tree2(p1, p2, n, DC, DC);
   if (tid < DC) {
     const double sg = p1[tid], sgu = p2[tid];
     g_scale[tid] = sgu;
