@@ -143,3 +143,38 @@ def build_flow(cfg):
         else:
             mods.append(bi.Roll(b["shift"]))
     return zf.Flow(bi.Chain(mods), latent=latent)
+
+
+# --- nested Flow (examples/deep_set.ipynb:318-328): a user module holding a Flow
+def make_deep_set_module():
+    """DeepSetFlow of the reference's deep-set example, restated on the
+    zenflow_amd module protocol: a conditioning network ``phi`` (here one
+    tanh Dense layer through ``Module.param``) and ``self.flow = Flow(...)``
+    built in ``setup()``, called as ``self.flow(y, c, train=train)`` and
+    ``self.flow.sample(c, seed=seed)``."""
+    import zenflow_amd as zf
+
+    class Phi(zf.Module):
+        def __call__(self, x):
+            w = self.param("kernel", lambda rng, shape: (0.5 * rng.standard_normal(shape)).astype(np.float32),
+                           (x.shape[1], 2))
+            b = self.param("bias", lambda rng, shape: np.zeros(shape, np.float32), (2,))
+            return np.tanh(np.asarray(x, np.float32) @ w + b).astype(np.float32)
+
+    class DeepSetFlow(zf.Module):
+        def __init__(self, bijectors):
+            self.bijectors = bijectors
+
+        def setup(self):
+            self.phi = Phi()
+            self.flow = zf.Flow(self.bijectors)
+
+        def __call__(self, x, y, train: bool = False):
+            c = self.phi(x)
+            return self.flow(y, c, train=train)
+
+        def sample(self, x, seed):
+            c = self.phi(x)
+            return self.flow.sample(c, seed=seed)
+
+    return DeepSetFlow

@@ -287,3 +287,54 @@ def test_apply_caches_program_by_content():
     f = np.isfinite(ref)
     assert_allclose(lp3[f], ref[f], rtol=2e-5, atol=2e-5)
     assert not np.allclose(lp3[f], lp1[f])
+
+
+def test_nested_flow_deep_set():
+    """DeepSetFlow (examples/deep_set.ipynb:318-328): the outer module calls
+    self.flow(y, c, train=train) and self.flow.sample(c, seed=seed); the
+    results equal a top-level Flow applied to the flow sub-tree bit for bit,
+    and train-mode batch-stats updates land at batch_stats/flow."""
+    from tests.flowcases import make_deep_set_module
+
+    DeepSetFlow = make_deep_set_module()
+    m = DeepSetFlow(bi.rolling_spline_coupling(2, layers=(64,) * 3))
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((1000, 3)).astype(np.float32)
+    y = (0.5 + 0.1 * rng.standard_normal((1000, 2))).astype(np.float32)
+    v = m.init(KEY, x, y)
+    _, upd = m.apply(v, x, y, train=True, mutable=["batch_stats"])
+    assert sorted(upd["batch_stats"]) == ["flow"]
+    v = {"params": v["params"], "batch_stats": upd["batch_stats"]}
+    lp = m.apply(v, x, y)
+    c = m.apply(v, x, method=lambda mod, x: mod.phi(x))
+    sub = {"params": v["params"]["flow"], "batch_stats": v["batch_stats"]["flow"]}
+    top = Flow(m.bijectors)
+    assert np.array_equal(lp, top.apply(sub, y, c), equal_nan=True)
+    # train-mode update of the nested flow == the top-level one
+    _, u_top = top.apply(sub, y, c, train=True, mutable=["batch_stats"])
+    _, u_nest = m.apply(v, x, y, train=True, mutable=["batch_stats"])
+    for path in [("bijectors_0", "xmin_0"), ("bijectors_1", "BatchNorm_0", "mean")]:
+        a, b = u_top["batch_stats"]["bijector"], u_nest["batch_stats"]["flow"]["bijector"]
+        for k in path:
+            a, b = a[k], b[k]
+        assert np.array_equal(a, b)
+    s_nest = m.apply(v, x, seed=3, method="sample")
+    s_top = top.apply(sub, c, seed=3, method="sample")
+    assert s_nest.shape == (1000, 2) and np.array_equal(s_nest, s_top, equal_nan=True)
+
+
+def test_bijector_apply_caches_program():
+    """Bijector-level apply (Chain / NSC) packs the weights once per distinct
+    variables content, as Flow does."""
+    ch = bi.rolling_spline_coupling(2, layers=(32, 32))
+    x = (0.5 + 0.1 * np.random.default_rng(1).standard_normal((256, 2))).astype(np.float32)
+    v = ch.init(KEY, x, None)
+    _, upd = ch.apply(v, x, None, train=True, mutable=["batch_stats"])
+    v = {"params": v["params"], "batch_stats": upd["batch_stats"]}
+    y1, ld1 = ch.apply(v, x, None)
+    assert len(ch._programs) == 1
+    y2, ld2 = ch.apply(v, x, None)
+    assert len(ch._programs) == 1 and np.array_equal(y1, y2) and np.array_equal(ld1, ld2)
+    xi = ch.apply(v, y1, None, method="inverse")
+    assert len(ch._programs) == 1
+    assert_allclose(xi, x, atol=2e-5)

@@ -139,3 +139,67 @@ def test_variables_npz_roundtrip(tmp_path):
         assert a[k].dtype == b[k].dtype and np.array_equal(a[k], b[k], equal_nan=True)
     with pytest.raises(ValueError):
         flatten_variables({"a/b": np.zeros(1)})
+
+
+def test_nested_flow_init_layout():
+    """A Flow held by an outer module (examples/deep_set.ipynb:318-328) gets
+    its variables under the attribute name, as flax.linen names submodules:
+    params/{phi, flow/bijector/...}, batch_stats/flow/bijector/...; the flow
+    sub-tree has the layout a top-level Flow.init would give."""
+    from tests.flowcases import make_deep_set_module
+
+    DeepSetFlow = make_deep_set_module()
+    m = DeepSetFlow(bi.rolling_spline_coupling(2, layers=(32,) * 3))
+    x = np.zeros((7, 3), np.float32)
+    y = np.full((7, 2), 0.5, np.float32)
+    v = m.init(PRNGKey(0), x, y)
+    assert sorted(v) == ["batch_stats", "params"]
+    assert sorted(v["params"]) == ["flow", "phi"]
+    assert v["params"]["phi"]["kernel"].shape == (3, 2)
+    top = zf.Flow(bi.rolling_spline_coupling(2, layers=(32,) * 3)).init(PRNGKey(0), y, np.zeros((7, 2), np.float32))
+
+    def shapes(t):
+        return {k: shapes(s) if isinstance(s, dict) else np.shape(s) for k, s in t.items()}
+
+    assert shapes(v["params"]["flow"]) == shapes(top["params"])
+    assert shapes(v["batch_stats"]["flow"]) == shapes(top["batch_stats"])
+    assert m.flow.latent.dim == 2
+    # apply outside the GPU path still resolves the sub-scope before computing
+    from zenflow_amd.module import Scope, SubScope, scope_for, _tls
+
+    s = Scope(v, False, owner=m)
+    _tls.scope = s
+    try:
+        sub = scope_for(m.flow)
+        assert isinstance(sub, SubScope) and sub.path == ("flow",)
+        assert sub.variables["params"] is v["params"]["flow"]
+        assert scope_for(m) is s
+    finally:
+        _tls.scope = None
+
+
+def test_module_variable_updates():
+    """Module.variable: mutable collections land in the updates at the
+    module's path; a non-mutable collection refuses writes (flax rule)."""
+
+    class Counter(zf.Module):
+        def __call__(self):
+            n = self.variable("batch_stats", "n", lambda: np.zeros((), np.int64))
+            n.value = n.value + 1
+            n.value = n.value + 1  # a second write sees the first
+            return n.value
+
+    class Outer(zf.Module):
+        def setup(self):
+            self.count = Counter()
+
+        def __call__(self):
+            return self.count()
+
+    m = Outer()
+    v = m.init(PRNGKey(0))
+    assert v == {"batch_stats": {"count": {"n": 2}}}
+    out, upd = m.apply(v, mutable=["batch_stats"])
+    assert out == 4 and upd["batch_stats"]["count"]["n"] == 4 and v["batch_stats"]["count"]["n"] == 2
+    with pytest.raises(RuntimeError):
+        m.apply(v)

@@ -222,7 +222,14 @@ def ensure_device() -> None:
             "MI355X (gfx950) and has no CPU fallback."
         )
     dev = int(os.environ.get("LOCAL_RANK", os.environ.get("ZF_DEVICE", "0")))
-    dev = dev % device_count()
+    n = device_count()
+    if not 0 <= dev < n:
+        # one process per GPU: an oversubscribed or mis-masked launch would put
+        # two ranks on one device and fail later inside RCCL
+        raise RuntimeError(
+            f"zenflow_amd: device {dev} (LOCAL_RANK/ZF_DEVICE) is not visible; "
+            f"{n} HIP device(s) visible — launch at most one rank per GPU"
+        )
     check(load_library().zf_set_device(dev), "zf_set_device")
     _device_ready = True
 

@@ -13,8 +13,8 @@ from typing import Callable, Dict, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from . import _lib as L
-from .engine import Program
-from .module import Module, current_scope, lecun_normal
+from .engine import Program, cached_program
+from .module import Module, lecun_normal, scope_for
 
 __all__ = [
     "Bijector",
@@ -53,14 +53,18 @@ def _prep_c(c):
 
 def _run_forward(module, x, c, train):
     """Shared __call__ of every bijector: one program over this module's chain."""
-    scope = current_scope()
+    scope = scope_for(module)
+    if scope.initializing:  # inside an outer module's init: create variables only
+        shape = np.shape(x) if not isinstance(x, L.DeviceArray) else x.shape
+        scope.init_module(module, int(shape[1]), _c_dims(c))
+        return np.array(x, np.float32, copy=True), np.zeros(shape[0], np.float32)
     xd, x_dev = L.as_device(x)
     if xd.ndim != 2:
         raise ValueError(f"x must be 2-D (N, D), got shape {xd.shape}")
     cd, _ = _prep_c(c)
     D = xd.shape[1]
     Cd = 0 if cd is None else cd.shape[1]
-    prog = Program(module, scope.variables, D, Cd)
+    prog = cached_program(module, module, scope.variables, D, Cd, cached=not train)
     if train:
         update = "batch_stats" in scope.mutable
         if not update and _has_stats(module):
@@ -78,12 +82,14 @@ def _run_forward(module, x, c, train):
 
 
 def _run_inverse(module, x, c):
-    scope = current_scope()
+    scope = scope_for(module)
+    if scope.initializing:
+        return np.array(x, np.float32, copy=True)
     xd, x_dev = L.as_device(x)
     if xd.ndim != 2:
         raise ValueError(f"x must be 2-D (N, D), got shape {xd.shape}")
     cd, _ = _prep_c(c)
-    prog = Program(module, scope.variables, xd.shape[1], 0 if cd is None else cd.shape[1])
+    prog = cached_program(module, module, scope.variables, xd.shape[1], 0 if cd is None else cd.shape[1])
     out = prog.inverse(xd, cd)
     return out if x_dev else out.numpy()
 

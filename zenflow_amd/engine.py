@@ -24,6 +24,13 @@ from . import _lib as L
 from ._lib import DeviceArray, check
 from .module import get_path, set_path
 
+try:  # fast content digest when available; stdlib otherwise
+    import xxhash as _xxhash
+except ImportError:  # pragma: no cover - depends on the environment
+    _xxhash = None
+import hashlib
+from collections import OrderedDict
+
 BN_MOMENTUM = 0.99  # flax.linen.BatchNorm default
 BN_EPS = 1e-5
 
@@ -388,3 +395,47 @@ def _latent_code(latent) -> Tuple[int, float]:
 
 def to_host_like(arr: DeviceArray, like_device: bool):
     return arr if like_device else arr.numpy()
+
+
+def _digest(tree) -> str:
+    """Content digest of a variables tree: paths, shapes, dtypes and bytes."""
+    h = _xxhash.xxh3_128() if _xxhash is not None else hashlib.blake2b(digest_size=16)
+
+    def walk(node, path):
+        if isinstance(node, dict):
+            for k in sorted(node):
+                walk(node[k], path + "/" + str(k))
+            return
+        a = np.ascontiguousarray(np.asarray(node))
+        h.update(f"{path}:{a.dtype.str}:{a.shape};".encode())
+        h.update(memoryview(a).cast("B"))
+
+    walk(tree, "")
+    return h.hexdigest()
+
+
+PROGRAM_CACHE_SIZE = 4
+
+
+def cached_program(owner, module, variables, D: int, C: int, latent=None, cached: bool = True) -> "Program":
+    """The device program of ``module`` for these variables, cached on
+    ``owner`` per (content digest of the variables, D, C, latent) so that
+    repeated ``apply(variables, x)`` calls pack and upload the weights once;
+    a digest (xxh3 over every leaf's bytes, ~0.1 ms/MB) rather than object
+    identity, because numpy leaves can be changed in place.  Train-mode
+    calls (``cached=False``) write batch statistics into their program and
+    never share it."""
+    if not cached:
+        return Program(module, variables, D, C, latent=latent)
+    key = (_digest(variables), int(D), int(C), type(latent).__name__,
+           getattr(latent, "peakness", None), getattr(latent, "_dim", None))
+    cache = owner.__dict__.setdefault("_programs", OrderedDict())
+    prog = cache.get(key)
+    if prog is None:
+        prog = Program(module, variables, D, C, latent=latent)
+        cache[key] = prog
+        while len(cache) > PROGRAM_CACHE_SIZE:
+            cache.popitem(last=False)
+    else:
+        cache.move_to_end(key)
+    return prog

@@ -2,17 +2,15 @@
 
 from __future__ import annotations
 
-from collections import OrderedDict
 from typing import Any, Dict, Optional, Union
 
 import numpy as np
-import xxhash
 
 from . import _lib as L
 from .bijectors import Bijector, Chain, _has_stats, _prep_c
 from .distributions import Beta, Distribution
-from .engine import Program
-from .module import Module, current_scope
+from .engine import Program, cached_program
+from .module import Module, scope_for
 from .random import PRNGKey, key_to_seed
 
 __all__ = ["Flow", "BoundFlow"]
@@ -29,7 +27,15 @@ class Flow(Module):
     # -- FLAX-style methods ----------------------------------------------------
     def __call__(self, x, c=None, *, train: bool = False):
         """log_prob of the samples (flow.py:22-48); NaN -> -inf."""
-        scope = current_scope()
+        scope = scope_for(self)
+        if scope.initializing:  # inside an outer module's init: create variables only
+            shape = np.shape(x) if not isinstance(x, L.DeviceArray) else x.shape
+            if len(shape) != 2:
+                raise ValueError(f"x must be 2-D (N, D), got {shape}")
+            from .bijectors import _c_dims
+
+            scope.init_module(self, int(shape[1]), _c_dims(c))
+            return np.zeros(shape[0], np.float32)
         xd, x_dev = L.as_device(x)
         if xd.ndim != 2:
             raise ValueError(f"x must be 2-D (N, D), got {xd.shape}")
@@ -54,7 +60,7 @@ class Flow(Module):
     def sample(self, conditions_or_size: Union[Any, int], *, seed: int = 0):
         """Samples from the learned distribution (flow.py:50-78): latent draw,
         then the bijector inverse on the GPU."""
-        scope = current_scope()
+        scope = scope_for(self)
         if isinstance(conditions_or_size, (int, np.integer)):
             size, c = int(conditions_or_size), None
         else:
@@ -62,6 +68,8 @@ class Flow(Module):
             size = c.shape[0]
         if self.latent.dim is None:
             raise ValueError("latent dim unknown: call log_prob (or init) first")
+        if scope.initializing:
+            return np.zeros((size, self.latent.dim), np.float32)
         cd, c_dev = _prep_c(c)
         if cd is not None and cd.shape[0] != size:
             raise ValueError("conditions must have one row per sample")
@@ -73,7 +81,7 @@ class Flow(Module):
         """Per-bijector intermediates (flow.py:80-95), one segment launch each."""
         if not isinstance(self.bijector, Chain):
             raise ValueError("only for Chain bijector")
-        scope = current_scope()
+        scope = scope_for(self)
         xd, _ = L.as_device(x)
         cd, _ = _prep_c(c)
         prog = self._program(scope.variables, xd.shape[1], 0 if cd is None else cd.shape[1])
@@ -96,8 +104,6 @@ class Flow(Module):
         return results
 
     # -- helpers ----------------------------------------------------------------
-    _CACHE_SIZE = 4
-
     def _program(self, variables, D, C, cached: bool = True) -> Program:
         """The device program for these variables.  Eval-mode programs are
         cached per (content digest of the variables, D, C, latent), so repeated
@@ -106,20 +112,7 @@ class Flow(Module):
         identity, because numpy leaves can be changed in place.  Train-mode
         calls write batch statistics into their program and never share it."""
         sub = {k: (v or {}).get("bijector", {}) for k, v in (variables or {}).items()}
-        if not cached:
-            return Program(self.bijector, sub, D, C, latent=self.latent)
-        key = (_digest(sub), int(D), int(C), type(self.latent).__name__,
-               getattr(self.latent, "peakness", None), self.latent._dim)
-        cache = self.__dict__.setdefault("_programs", OrderedDict())
-        prog = cache.get(key)
-        if prog is None:
-            prog = Program(self.bijector, sub, D, C, latent=self.latent)
-            cache[key] = prog
-            while len(cache) > self._CACHE_SIZE:
-                cache.popitem(last=False)
-        else:
-            cache.move_to_end(key)
-        return prog
+        return cached_program(self, self.bijector, sub, D, C, self.latent, cached)
 
     def _init_variables(self, gen, D, C, params, stats):
         p: Dict = {}
@@ -139,23 +132,6 @@ class Flow(Module):
         if self.latent._dim is None:
             self.latent._dim = dim
         return BoundFlow(self._program(variables, dim, cond_dim))
-
-
-def _digest(tree) -> str:
-    """Content digest of a variables tree: paths, shapes, dtypes and bytes."""
-    h = xxhash.xxh3_128()
-
-    def walk(node, path):
-        if isinstance(node, dict):
-            for k in sorted(node):
-                walk(node[k], path + "/" + str(k))
-            return
-        a = np.ascontiguousarray(np.asarray(node))
-        h.update(f"{path}:{a.dtype.str}:{a.shape};".encode())
-        h.update(memoryview(a).cast("B"))
-
-    walk(tree, "")
-    return h.hexdigest()
 
 
 class BoundFlow:

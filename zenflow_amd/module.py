@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import copy
 import threading
-from typing import Any, Dict, Optional
+from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import numpy as np
 
@@ -21,9 +21,11 @@ _tls = threading.local()
 
 
 class Scope:
-    """Variables bound for one ``apply`` call, plus the collections it may mutate."""
+    """Variables bound for one ``apply`` (or ``init``) call of the OUTERMOST
+    module, plus the collections it may mutate.  Child modules see a
+    ``SubScope`` of it at their attribute path (``scope_for``)."""
 
-    def __init__(self, variables: Dict[str, Any], mutable):
+    def __init__(self, variables: Dict[str, Any], mutable, owner=None, initializing: bool = False, rng=None):
         self.variables = variables or {}
         if mutable is True:
             mutable = ["params", "batch_stats"]
@@ -31,10 +33,76 @@ class Scope:
             mutable = [mutable]
         self.mutable = list(mutable or [])
         self.updates: Dict[str, Any] = {}
-        self.initializing = False
+        self.owner = owner
+        self.initializing = initializing
+        self.rng = rng  # numpy Generator while initializing
+        self.path: Tuple[str, ...] = ()
 
     def collection(self, name: str) -> Dict[str, Any]:
         return self.variables.get(name, {}) or {}
+
+    def put(self, col: str, name: str, value) -> None:
+        """Create a variable while initializing."""
+        self.variables.setdefault(col, {})[name] = value
+
+    def init_module(self, module, D: int, C: int) -> None:
+        """Initializing: create ``module``'s own variables (its
+        ``_init_variables`` for inputs of D dims and C conditions) here."""
+        p: Dict[str, Any] = {}
+        st: Dict[str, Any] = {}
+        module._init_variables(self.rng, D, C, p, st)
+        for k, v in p.items():
+            self.put("params", k, v)
+        for k, v in st.items():
+            self.put("batch_stats", k, v)
+        module._on_init(D, C)
+
+
+class _Updates:
+    """``scope.updates[col] = tree`` of a child: written into the root's
+    updates at the child's path, on a copy of the whole collection (FLAX
+    returns the full updated collection)."""
+
+    def __init__(self, root: Scope, path):
+        self.root, self.path = root, tuple(path)
+
+    def __setitem__(self, col: str, value) -> None:
+        if col not in self.root.updates:
+            self.root.updates[col] = copy.deepcopy(self.root.variables.get(col, {}) or {})
+        set_path(self.root.updates[col], self.path, value)
+
+    def __contains__(self, col) -> bool:
+        return col in self.root.updates
+
+
+class SubScope:
+    """A child module's view of the root scope: every collection at ``path``
+    (e.g. ``variables["params"]["flow"]`` for ``self.flow`` of an outer
+    module, as flax.linen names submodules by attribute)."""
+
+    def __init__(self, root: Scope, path):
+        self.root, self.path = root, tuple(path)
+        self.mutable = root.mutable
+        self.initializing = root.initializing
+        self.rng = root.rng
+        self.updates = _Updates(root, self.path)
+
+    @property
+    def variables(self) -> Dict[str, Any]:
+        out = {}
+        for col, tree in self.root.variables.items():
+            v = get_path(tree or {}, self.path)
+            if v is not None:
+                out[col] = v
+        return out
+
+    def collection(self, name: str) -> Dict[str, Any]:
+        return get_path(self.root.variables.get(name, {}) or {}, self.path) or {}
+
+    def put(self, col: str, name: str, value) -> None:
+        set_path(self.root.variables.setdefault(col, {}), self.path + (name,), value)
+
+    init_module = Scope.init_module
 
 
 def current_scope() -> Scope:
@@ -47,6 +115,25 @@ def current_scope() -> Scope:
     return s
 
 
+def scope_for(module) -> Union[Scope, SubScope]:
+    """The scope ``module`` sees: the root scope when it is the module that
+    ``apply``/``init`` was called on (or not a descendant of it), else the
+    sub-scope at its attribute path below that module — so a Flow held as
+    ``self.flow`` by an outer module reads ``variables[col]["flow"]``
+    (examples/deep_set.ipynb: ``self.flow(y, c, train=train)``)."""
+    s = current_scope()
+    if s.owner is None or module is s.owner:
+        return s
+    path = []
+    m = module
+    while m is not None and m is not s.owner:
+        path.append(m.__dict__.get("_zf_name"))
+        m = m.__dict__.get("_zf_parent")
+    if m is None or any(p is None for p in path):
+        return s
+    return SubScope(s, reversed(path))
+
+
 def _resolve_method(module, method):
     if method is None:
         return type(module).__call__
@@ -55,8 +142,45 @@ def _resolve_method(module, method):
     return method
 
 
+def _name_children(parent, name: str, value) -> None:
+    if isinstance(value, Module):
+        value.__dict__["_zf_parent"] = parent
+        value.__dict__["_zf_name"] = name
+    elif isinstance(value, (list, tuple)):
+        for i, v in enumerate(value):
+            if isinstance(v, Module):  # flax: <attr>_<i>
+                v.__dict__["_zf_parent"] = parent
+                v.__dict__["_zf_name"] = f"{name}_{i}"
+
+
 class Module:
-    """Base class: FLAX-like ``init`` and ``apply``."""
+    """Base class: FLAX-like ``init`` and ``apply``.
+
+    Submodules assigned as attributes (in ``__init__`` or in a ``setup()``
+    method, which runs lazily as in flax.linen) are named by their attribute
+    (``self.flow`` -> ``"flow"``, a list ``self.layers`` -> ``"layers_<i>"``)
+    and read their variables from that sub-tree when called inside the outer
+    module's ``apply``/``init``.  ``param``/``variable`` give user modules
+    their own variables."""
+
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if not name.startswith("_"):
+            _name_children(self, name, value)
+
+    def __getattr__(self, name):
+        # flax runs setup() lazily on first attribute access
+        d = self.__dict__
+        if not name.startswith("__") and not d.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
+            d["_zf_setup_done"] = True
+            self.setup()
+            return getattr(self, name)
+        raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
+
+    def _ensure_setup(self) -> None:
+        if not self.__dict__.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
+            self.__dict__["_zf_setup_done"] = True
+            self.setup()
 
     def init(self, rng, *args, method=None, **kwargs) -> Dict[str, Any]:
         """Create the variables (``params`` + ``batch_stats``) for the input shapes.
@@ -65,10 +189,23 @@ class Module:
         default initialisers (lecun_normal kernels, zero biases, BatchNorm
         scale 1 / bias 0 / mean 0 / var 1); ShiftBounds stats start at +-inf.
         ``rng`` may be ``zenflow_amd.random.PRNGKey(seed)``, an int or a
-        ``numpy.random.Generator``."""
+        ``numpy.random.Generator``.  A module that does not define its own
+        variables (a user module holding a Flow, say) runs ``method`` once in
+        initializing mode: each submodule creates its variables from the
+        inputs it is called with (outputs are placeholders, not computed)."""
         from .random import as_generator
 
         gen = as_generator(rng)
+        if type(self)._init_variables is Module._init_variables:
+            self._ensure_setup()
+            scope = Scope({}, True, owner=self, initializing=True, rng=gen)
+            prev = getattr(_tls, "scope", None)
+            _tls.scope = scope
+            try:
+                _resolve_method(self, method)(self, *args, **kwargs)
+            finally:
+                _tls.scope = prev
+            return {k: v for k, v in scope.variables.items() if v}
         x = args[0] if args else kwargs.get("x")
         c = args[1] if len(args) > 1 else kwargs.get("c")
         shape = np.shape(x)
@@ -91,8 +228,9 @@ class Module:
 
         With ``mutable`` (e.g. ``["batch_stats"]``) returns ``(out, updates)``
         as FLAX does."""
+        self._ensure_setup()
         fn = _resolve_method(self, method)
-        scope = Scope(variables, mutable)
+        scope = Scope(variables, mutable, owner=self)
         prev = getattr(_tls, "scope", None)
         _tls.scope = scope
         try:
@@ -109,12 +247,69 @@ class Module:
             return out, upd
         return out
 
+    # variables of user modules (flax.linen.Module.param / .variable) ---------
+    def param(self, name: str, init_fn: Callable, *init_args):
+        """``params`` variable ``name`` of this module: created by
+        ``init_fn(rng, *init_args)`` while initializing, read otherwise."""
+        s = scope_for(self)
+        cur = s.collection("params")
+        if name not in cur:
+            if not s.initializing:
+                raise KeyError(f"params/{'/'.join(s.path + (name,))} is missing from the variables")
+            s.put("params", name, init_fn(s.rng, *init_args))
+            cur = s.collection("params")
+        return cur[name]
+
+    def variable(self, col: str, name: str, init_fn: Callable, *init_args) -> "Variable":
+        """A mutable variable of collection ``col`` (e.g. ``batch_stats``)."""
+        s = scope_for(self)
+        if name not in s.collection(col):
+            if not s.initializing:
+                raise KeyError(f"{col}/{'/'.join(s.path + (name,))} is missing from the variables")
+            s.put(col, name, init_fn(*init_args))
+        return Variable(s, col, name)
+
     # subclasses --------------------------------------------------------------
     def _init_variables(self, gen, D, C, params, stats) -> None:
         pass
 
     def _on_init(self, D, C) -> None:
         pass
+
+
+class Variable:
+    """flax.core.scope.Variable: ``.value`` reads the bound variable; setting
+    it requires the collection to be mutable and lands in the updates."""
+
+    def __init__(self, scope, col: str, name: str):
+        self._scope, self._col, self._name = scope, col, name
+
+    @property
+    def value(self):
+        s = self._scope
+        root = s.root if isinstance(s, SubScope) else s
+        path = s.path if isinstance(s, SubScope) else ()
+        if self._col in root.updates:  # updated earlier in this call
+            tree = get_path(root.updates[self._col], path)
+            if tree is not None and self._name in tree:
+                return tree[self._name]
+        return s.collection(self._col)[self._name]
+
+    @value.setter
+    def value(self, v):
+        s = self._scope
+        if s.initializing:
+            s.put(self._col, self._name, v)
+            return
+        if self._col not in s.mutable:
+            raise RuntimeError(f"collection {self._col!r} is not mutable (pass mutable=[{self._col!r}])")
+        root = s.root if isinstance(s, SubScope) else s
+        path = s.path if isinstance(s, SubScope) else ()
+        # the latest value of the collection (an earlier update of this call included)
+        base = get_path(root.updates[self._col], path) if self._col in root.updates else None
+        tree = copy.deepcopy(base if base is not None else s.collection(self._col))
+        tree[self._name] = v
+        s.updates[self._col] = tree
 
 
 def lecun_normal(gen: np.random.Generator, fan_in: int, fan_out: int) -> np.ndarray:

@@ -13,8 +13,9 @@ Not reproducible offline (no JAX / optax here): jax.random's init and
 permutation streams (seeded numpy generators stand in) and optax's exact
 floating-point order; the optimiser restates optax's published update
 (scale_by_adam with nesterov for nadamw -> add_decayed_weights -> scale by
--learning_rate).  Gradients are checked against finite differences of the
-fp64 oracle (tests/test_gpu_train.py)."""
+-learning_rate).  Every gradient element is checked against float64
+autograd of the oracle's loss (oracle/zf_oracle_torch.py,
+tests/test_gpu_train.py::test_train_gradient_per_parameter)."""
 
 from __future__ import annotations
 
@@ -56,6 +57,9 @@ def adamw(learning_rate: float = 1e-3, b1: float = 0.9, b2: float = 0.999, eps: 
           weight_decay: float = 1e-4) -> Optimizer:
     return Optimizer(learning_rate, b1, b2, eps, weight_decay, False)
 
+
+# |sum(lp)| from which the fp32 sum of the reference's jnp.mean is infinite
+_F32_SUM_LIMIT = float(np.finfo(np.float32).max)
 
 DEFAULT_OPTIMIZER = nadamw  # train.py:13-16 (optax.nadamw when available)
 
@@ -121,7 +125,8 @@ class Trainer:
         check(L.load_library().zf_trainer_loss_grad_shard(
             self.handle, xd.ptr, None if cd is None else cd.ptr, xd.shape[0], self._global(xd.shape[0], global_rows),
             1 if update_stats else 0, self._loss.ptr, g.ptr, L.stream()), "zf_trainer_loss_grad")
-        return float(self._loss.numpy()[0]), g.numpy()
+        self._last_rows = self._global(xd.shape[0], global_rows)
+        return self._fp32_mean(float(self._loss.numpy()[0])), g.numpy()
 
     def grad_tree(self, grad_blob: np.ndarray) -> Dict[str, Any]:
         """Gradient blob -> FLAX ``params`` tree (like jax.grad's output)."""
@@ -133,11 +138,24 @@ class Trainer:
 
     def _step_rows(self, xptr: int, cptr: Optional[int], rows: int, global_rows: Optional[int] = None) -> None:
         """One step on ``rows`` device-resident rows (raw pointers; async)."""
+        self._last_rows = self._global(rows, global_rows)
         check(L.load_library().zf_trainer_step_shard(self.handle, xptr, cptr, rows, self._global(rows, global_rows),
                                                      self._loss.ptr, L.stream()), "zf_trainer_step")
 
     def last_loss(self) -> float:
-        return float(self._loss.numpy()[0])
+        return self._fp32_mean(float(self._loss.numpy()[0]))
+
+    def _fp32_mean(self, loss: float) -> float:
+        """The device loss is -sum(lp / B) in fp64; the reference's loss_fn
+        (train.py:70-72) is jnp.mean in fp32, whose sum overflows to +-inf once
+        |sum(lp)| leaves the fp32 range (two rows at finfo.min) — the same rule
+        as dist.nll_from_sum, applied to the global batch of the last call."""
+        from .dist import nll_from_sum
+
+        B = getattr(self, "_last_rows", None)
+        if B is None or loss != loss:
+            return loss
+        return nll_from_sum(-loss * B, B) if abs(loss * B) >= _F32_SUM_LIMIT else loss
 
     def variables(self) -> Dict[str, Any]:
         blob = np.empty_like(self.program.blob)
