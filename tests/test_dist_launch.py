@@ -77,15 +77,33 @@ def test_torchrun_style_env(tmp_path):
     assert not Path(res[0]["dir"]).exists()  # rank 0 cleaned up
 
 
-def test_bench_gpus2_spawns_two_ranks():
-    """`python bench.py --gpus 2` with no launcher starts two ranks itself;
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_spawns_ranks(world):
+    """`python bench.py --gpus N` with no launcher starts N ranks itself;
     on this GPU-less host each reaches the no-device error of the product
     path (no CPU fallback)."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ZF_RDZV_DIR")}
-    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "1", "--warmup", "0"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
-    assert p.stderr.count("no HIP device is visible") == 2, p.stderr[-2000:]
+    assert p.stderr.count("no HIP device is visible") == world, p.stderr[-2000:]
+
+
+@pytest.mark.parametrize("config,world,batch", [("cfg5", 8, 1 << 23), ("cfg2", 8, 1 << 23), ("cfg2", 1, 1 << 20),
+                                                ("cfg5", 2, 1 << 21)])
+def test_bench_dry_run_global_batch(config, world, batch):
+    """The scaling run's shapes: cfg5 at --gpus 8 is
+    BASELINE's 2^23-row batch sharded 2^20 rows per GPU (weak scaling); the
+    ranks rendezvous, rank 0 prints the config, no GPU is touched."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ZF_RDZV_DIR")}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--config", config, "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == batch
+    assert out["config"]["rows_per_gpu"] == 1 << 20
 
 
 def test_bench_rejects_mismatched_world():
