@@ -179,7 +179,7 @@ def spline_kernel_roofline(M, N, K, steps):
     y = DeviceArray((M, N))
     ld = DeviceArray((M,))
     xi = DeviceArray((M, N))
-    out = {}
+    out = {"check": None}
     for tag in ("forward", "inverse", "normalize"):
         def run():
             if tag == "normalize":
@@ -206,6 +206,22 @@ def spline_kernel_roofline(M, N, K, steps):
         gbs = nbytes / t / 1e9
         out[tag] = {"kernel": kname, "shape": [M, N, K], "us": t * 1e6, "alg_bytes": nbytes,
                     "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
+    # outputs of the timed launches at the timed shape vs the oracle, on a
+    # strided row sample (the full-shape test is tests/test_gpu_rqs.py)
+    from oracle import zf_oracle as O
+
+    rows = sample_rows(M, 8192)
+    hx, hdx, hdy, hsl = x.numpy()[rows], dx.numpy()[rows], dy.numpy()[rows], sl.numpy()[rows]
+    yr, ldr = O.rqs_forward(hx, hdx, hdy, hsl)
+    xr = O.rqs_inverse(y.numpy()[rows], hdx, hdy, hsl)
+    gy, gld, gxi = y.numpy()[rows], ld.numpy()[rows], xi.numpy()[rows]
+
+    def err(a, b):
+        f = np.isfinite(a) & np.isfinite(b)
+        return {"max_abs_err": float(np.abs(a[f] - b[f]).max()) if f.any() else None,
+                "finiteness_mismatches": int((np.isfinite(a) != np.isfinite(b)).sum())}
+
+    out["check"] = {"rows": int(len(rows)), "y": err(gy, yr), "log_det": err(gld, ldr), "inverse": err(gxi, xr)}
     return out
 
 

@@ -125,6 +125,31 @@ def test_rqs_parity(K, N):
     assert_allclose(xi[fin], xr[fin], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("K", [16, 32])
+def test_rqs_parity_bench_shape(K):
+    """K1 at the bench's timed shape — one cfg2 coupling over 2^20 rows x 2
+    transformed dims (bench.py spline_kernel) — against the oracle on every
+    row: y, log_det, and the inverse of the reference's y."""
+    u = _zu()
+    rng = np.random.default_rng(K)
+    M = 1 << 20
+    dx, dy, sl = random_params(rng, M, 2, K, scale=1.5)
+    x = rng.uniform(-0.05, 1.05, size=(M, 2)).astype(F32)
+    y, ld = u.rational_quadratic_spline_forward(x, dx, dy, sl)
+    yr, ldr = O.rqs_forward(x, dx, dy, sl)
+    fin = np.isfinite(yr)
+    assert np.array_equal(fin, np.isfinite(y))
+    assert_allclose(y[fin], yr[fin], rtol=2e-6, atol=2e-6)
+    finl = np.isfinite(ldr)
+    assert np.array_equal(finl, np.isfinite(ld))
+    assert_allclose(ld[finl], ldr[finl], rtol=1e-5, atol=1e-5)
+    xi = u.rational_quadratic_spline_inverse(yr, dx, dy, sl)
+    xr = O.rqs_inverse(yr, dx, dy, sl)
+    fin = np.isfinite(xr)
+    assert np.array_equal(fin, np.isfinite(xi))
+    assert_allclose(xi[fin], xr[fin], rtol=1e-5, atol=1e-5)
+
+
 def test_rqs_edge_cases():
     """Sliver idx == K (fill-mode gather -> NaN), x == 1 (OOB identity), NaN x,
     empty batch."""

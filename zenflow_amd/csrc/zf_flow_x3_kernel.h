@@ -81,6 +81,15 @@ struct XT<2> {
 constexpr int kWideSched = 3;
 
 constexpr int kX3Waves = 4;  // waves per block: 128 samples
+
+// Tuning-only phase trace (a separate build with -DZF_X3_TRACE=1, never the
+// shipped library): each wave sums s_memtime ticks per phase and writes them
+// at exit (lane 0, vector stores) to the buffer zf_x3_trace_set_k* installs.
+#ifdef ZF_X3_TRACE
+constexpr int kX3TraceSlots = 16;
+__device__ unsigned long long* x3_trace_buf;
+#define X3T_NOW() __builtin_amdgcn_s_memtime()
+#endif
 // Bytes of one weight group = one 32-row input tile: [s][out tile][part] x 1 KiB.
 template <int NT>
 constexpr int group_bytes(int NOUT) { return 2 * NOUT * NT * 1024; }
@@ -370,6 +379,9 @@ struct X3Pipe {
   int g;        // index of that group within the current NSC
   X3Span span;  // current NSC's group stream
   int wave;
+#ifdef ZF_X3_TRACE
+  unsigned long long tbar;  // ticks spent in the per-group DMA wait + barrier
+#endif
 };
 
 // DMA the group after group p.g (the next one of this NSC, or group 0 of
@@ -404,8 +416,14 @@ template <int NT, int T, int NOUT, int Q, bool SW, bool OACT>
 __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                         floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
                                         int hh, float isc, float us, int act) {
+#ifdef ZF_X3_TRACE
+  const unsigned long long tb0 = X3T_NOW();
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#ifdef ZF_X3_TRACE
+  p.tbar += X3T_NOW() - tb0;
+#endif
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
   if (bias != nullptr) {
     floatx16 bt[NOUT];
@@ -454,8 +472,14 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
                                              int hh, typename XT<NT>::E (&cs)[NT], float isc, float us,
                                              int act) {
   using E = typename XT<NT>::E;
+#ifdef ZF_X3_TRACE
+  const unsigned long long tb0 = X3T_NOW();
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#ifdef ZF_X3_TRACE
+  p.tbar += X3T_NOW() - tb0;
+#endif
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
   floatx16 bt[NOUT];
   if constexpr (HASB) {
@@ -608,6 +632,23 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   pipe.nxt = lds + kBuf;
   pipe.g = 0;
   pipe.wave = wave;
+#ifdef ZF_X3_TRACE
+  // slots: 0 start->first NSC, 1 layer 0, 2 hidden layers, 3 hidden->last
+  // transition, 4 last layer, 5 spline, 6 epilogue, 7 barrier waits (inside
+  // 2 and 4), 8 total, 9 couplings, 10 other ops
+  unsigned long long tacc[kX3TraceSlots] = {};
+  pipe.tbar = 0;
+  const unsigned long long t_begin = X3T_NOW();
+  unsigned long long t_last = t_begin;
+#define X3T(k)                                   \
+  {                                              \
+    const unsigned long long t_ = X3T_NOW();     \
+    tacc[k] += t_ - t_last;                      \
+    t_last = t_;                                 \
+  }
+#else
+#define X3T(k)
+#endif
   {  // group 0 of the first NSC in execution order goes out now
     int first = -1;
     const int nq = op_end - op_begin;
@@ -628,7 +669,12 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
       shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
+      X3T(10);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
+      X3T(0);
+#ifdef ZF_X3_TRACE
+      tacc[9] += 1;
+#endif
       pipe.span = make_span<NT, T, INV>(F, oi, op_begin, op_end);
       pipe.g = 0;
       floatx16 hb[T];
@@ -651,6 +697,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
       // +1.2% d8; nothing to arbitrate at hidden 256, one wave per SIMD).
       if constexpr (T == 4) __builtin_amdgcn_s_setprio(2);
+      X3T(1);
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;
@@ -689,6 +736,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           }
         }
       }
+      X3T(2);
       // Last Dense (:346-347), one pair of transformed dims at a time: lane
       // half h, tile o, register r = parameter 16*o + r of dim 2*pair + h.
       const int dt = op.dt;
@@ -715,6 +763,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
         for (int o = 0; o < TL; ++o)
           pa[o] = kSeed ? bias_acc(bl + o * 32, hh) : (kSeedScaled ? bias_acc(bl + o * 32, hh) * lius : floatx16{0});
+        X3T(3);
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
@@ -728,6 +777,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           for (int o = 0; o < TL; ++o) pa[o] *= lus;
         }
         if constexpr (T == 4) __builtin_amdgcn_s_setprio(0);
+        X3T(4);
         float P[NPV];
 #pragma unroll
         for (int o = 0; o < TL; ++o)
@@ -791,11 +841,23 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         }
       }
       if (!INV) ld = ld + ldn;  // Chain: log_det += ld (bijectors.py:110)
+      X3T(5);
     }
   }
 
   flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, nparts, y_out,
                     ld_out, s_part);
+#ifdef ZF_X3_TRACE
+  X3T(6);
+  tacc[7] = pipe.tbar;
+  tacc[8] = t_last - t_begin;
+  if (lane == 0 && x3_trace_buf != nullptr) {
+    unsigned long long* o = x3_trace_buf + ((long long)blockIdx.x * NW + wave) * kX3TraceSlots;
+#pragma unroll
+    for (int k = 0; k < kX3TraceSlots; ++k) o[k] = tacc[k];
+  }
+#endif
+#undef X3T
 }
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool OACT>
