@@ -98,6 +98,12 @@ __device__ __forceinline__ void bias_tile(const float* __restrict__ bt, int hh, 
 // The same bias tile as an accumulator initialiser: a layer's MFMAs then
 // accumulate onto its bias (no separate add, no zero fill).
 __device__ __forceinline__ floatx16 bias_acc(const float* __restrict__ bt, int hh) {
+#if defined(ZF_X3_ABL) && ZF_X3_ABL == 7  // tuning ablation 7: no small-parameter loads (wrong results)
+  floatx16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.01f * (r + hh);
+  return z;
+#endif
   floatx4 b[4];
   bias_tile(bt, hh, b);
   floatx16 a;
@@ -206,11 +212,18 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
     float v = 0.f;
     if (k < dc) v = xs[wrap(dt + k + rot, D) * 32 + s];
     else if (k < DC) v = valid ? cin[row * C + (k - dc)] : 0.f;
+#if defined(ZF_X3_ABL) && ZF_X3_ABL == 7
+    const float u = (v - 0.1f) * 1.1f + 0.01f;
+#pragma unroll
+    for (int o = 0; o < T; ++o)
+      hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(0.01f * (o + lane), u, hb[o], 0, 0, 0);
+#else
     const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
     const float* w0 = blob + op.w[0] + ks * 64 + lane;
 #pragma unroll
     for (int o = 0; o < T; ++o)
       hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
+#endif
   }
   // swish of tiles [0, swish_tiles): the bf16x3 kernel defers the others into
   // the next layer's MFMA stream

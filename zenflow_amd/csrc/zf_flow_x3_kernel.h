@@ -80,11 +80,18 @@ struct XT<2> {
 // per MFMA (measured +4-5% at cfg5; at T = 4 both were neutral to -12%).
 constexpr int kWideSched = 3;
 
-constexpr int kX3Waves = 4;  // waves per block: 128 samples
+#ifndef ZF_X3_WAVES
+#define ZF_X3_WAVES 4
+#endif
+constexpr int kX3Waves = ZF_X3_WAVES;  // waves per block: 32 samples each
+static_assert(kX3Waves % 4 == 0, "whole 128-row NLL partial slots per block");
 
 // Tuning-only phase trace (a separate build with -DZF_X3_TRACE=1, never the
 // shipped library): each wave sums s_memtime ticks per phase and writes them
 // at exit (lane 0, vector stores) to the buffer zf_x3_trace_set_k* installs.
+#ifndef ZF_X3_ABL
+#define ZF_X3_ABL 0  // tuning-only ablations (wrong results), never set in the shipped build
+#endif
 #ifdef ZF_X3_TRACE
 constexpr int kX3TraceSlots = 16;
 __device__ unsigned long long* x3_trace_buf;
@@ -367,6 +374,9 @@ __device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int o
 // global_load_lds_dwordx4 per wave: wave-uniform LDS base, lane*16 implied)
 // spread over the block's waves.
 __device__ __forceinline__ void x3_dma(const char* __restrict__ src, char* dst, int pieces, int wave, int lane) {
+#if ZF_X3_ABL == 5  // tuning ablation 5: a quarter of the weight stream (wrong results)
+  pieces = (pieces + 3) / 4;
+#endif
   for (int p = wave; p < pieces; p += kX3Waves)
     __builtin_amdgcn_global_load_lds((const void*)(src + (p << 10) + lane * 16),
                                      (__attribute__((address_space(3))) void*)(dst + (p << 10)), 16, 0, 0);
@@ -390,6 +400,9 @@ template <int NT, int T>
 __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
   constexpr int kHid = group_bytes<NT>(T);
   const int g = p.g + 1;
+#if ZF_X3_ABL == 6  // tuning ablation 6: the stream stops after each NSC's first two groups (real weights stay; wrong results)
+  if (g > 1 && g < p.span.G) return;
+#endif
   long long off;
   int pieces;
   if (g < p.span.nhid) {
@@ -475,8 +488,10 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 #ifdef ZF_X3_TRACE
   const unsigned long long tb0 = X3T_NOW();
 #endif
+#if ZF_X3_ABL != 3  // tuning ablation 3: no per-group DMA wait / barrier (wrong results)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#endif
 #ifdef ZF_X3_TRACE
   p.tbar += X3T_NOW() - tb0;
 #endif
@@ -489,21 +504,35 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   const char* lb = p.cur + lane * 16;
   E s1[NT];
   splitk<NT, 1>(hb[Q], s1);
+#if ZF_X3_ABL == 1  // tuning ablation 1: one A fragment per step (no per-tile LDS reads; wrong results)
+  E a1[NT];
+  load_frag<NT>(lb, a1);
+#endif
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
+#if ZF_X3_ABL == 1
+    acc[o] = mfma_split<NT>(a1, cs, acc[o]);
+#else
     E a[NT];
     load_frag<NT>(lb + ((o * NT) << 10), a);
     acc[o] = mfma_split<NT>(a, cs, acc[o]);
+#endif
   }
   if constexpr (Q + 1 < T) {
+#if ZF_X3_ABL != 2  // tuning ablation 2: no swish inside the group steps (wrong results)
     if constexpr (!OACT) x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
+#endif
     splitk<NT, 0>(hb[Q + 1], cs);
   }
 #pragma unroll
   for (int o = 0; o < NOUT; ++o) {
+#if ZF_X3_ABL == 1
+    acc[o] = mfma_split<NT>(a1, s1, acc[o]);
+#else
     E a[NT];
     load_frag<NT>(lb + (((NOUT + o) * NT) << 10), a);
     acc[o] = mfma_split<NT>(a, s1, acc[o]);
+#endif
   }
   if constexpr (HASB) {
 #pragma unroll
@@ -515,17 +544,79 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   p.g += 1;
 }
 
+#ifdef ZF_X3_EXP
+// Experimental (tuning builds): the group's A fragments all read from LDS at
+// the step's start (2 x NOUT x NT ds_read_b128, counted waits), so the MFMAs
+// do not wait on an LDS round trip per (k-step, tile); ZF_X3_EXP >= 2 also
+// interleaves the step's VALU evenly between its MFMAs.
+template <int NT, int T, int NOUT, int Q, bool HASB, bool OACT>
+__device__ __forceinline__ void x3_step_up(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                           floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                           int hh, typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
+  using E = typename XT<NT>::E;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+  floatx16 bt[NOUT];
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+  }
+  const char* lb = p.cur + lane * 16;
+  E fa[2][NOUT][NT];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) load_frag<NT>(lb + (((s2 * NOUT + o) * NT) << 10), fa[s2][o]);
+  E s1[NT];
+  splitk<NT, 1>(hb[Q], s1);
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) acc[o] = mfma_split<NT>(fa[0][o], cs, acc[o]);
+  if constexpr (Q + 1 < T) {
+    if constexpr (!OACT) x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
+    splitk<NT, 0>(hb[Q + 1], cs);
+  }
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) acc[o] = mfma_split<NT>(fa[1][o], s1, acc[o]);
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+  }
+#if ZF_X3_EXP >= 2
+  {
+    constexpr int kM = 2 * NOUT * XT<NT>::kProd;
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * NOUT * NT, 0);
+#pragma unroll
+    for (int i = 0; i < kM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+    }
+  }
+#endif
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+#endif
+
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
 template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
                                               typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
+#ifdef ZF_X3_EXP
+#define X3_STEP x3_step_up
+#else
+#define X3_STEP x3_step_pipe
+#endif
   if constexpr (Q + 1 < T) {
-    x3_step_pipe<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
+    X3_STEP<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
     x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   } else {
-    x3_step_pipe<NT, T, NOUT, Q, HASB, OACT>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
+    X3_STEP<NT, T, NOUT, Q, HASB, OACT>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   }
+#undef X3_STEP
 }
 
 // A whole streamed Dense layer: T groups (one per input tile).
@@ -592,7 +683,11 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // all tiles before the layer's groups instead of tile by tile inside them
 // (a switch inside the pipelined steps spilled 110-130 VGPRs at 3 waves).
 template <int T, int K, bool PAIRS>
+#ifdef ZF_X3_EXP
+constexpr int x3_occupancy() { return T == 8 ? 1 : 2; }
+#else
 constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
+#endif
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT>
 __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
@@ -696,7 +791,9 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
       // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
       // +1.2% d8; nothing to arbitrate at hidden 256, one wave per SIMD).
+#if ZF_X3_ABL != 4  // tuning ablation 4: no issue priority
       if constexpr (T == 4) __builtin_amdgcn_s_setprio(2);
+#endif
       X3T(1);
       for (int l = 1; l < op.n_hidden; ++l) {
         floatx16 acc[T];
@@ -845,7 +942,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
     }
   }
 
-  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, 1, nparts, y_out,
+  flow_epilogue<NW>(F, xs, s, hh, lane, wave, rot, D, row, valid, ld, lp_out, block_partial, NW / 4, nparts, y_out,
                     ld_out, s_part);
 #ifdef ZF_X3_TRACE
   X3T(6);
@@ -866,7 +963,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
   const long long grid = (a.N + rows - 1) / rows;
   if (grid > 0x7fffffffLL) return einval("N too large");
   constexpr int TL = ONE ? (3 * K - 1 + 31) / 32 : (3 * K - 1 + 15) / 16;
-  const size_t lds = x3_lds_bytes(T > TL ? T : TL, a.D, NT);
+  size_t lds = (size_t)2 * group_bytes<NT>(T > TL ? T : TL) + (size_t)kX3Waves * 32 * a.D * 4 +
+               kX3Waves * sizeof(double);
+#ifdef ZF_X3_TRACE
+  if (const char* pad = std::getenv("ZF_X3_LDS_PAD")) lds += (size_t)std::atoi(pad) * 1024;  // occupancy probe
+#endif
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
     hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true, OACT>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
