@@ -603,7 +603,22 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   }
   std::vector<uint16_t> x3s;
   const int NT = zf::x3_scheme();
-  if (x3 && zf::x3_lds_bytes(zf::x3_buf_tiles(desc, T, x3K), desc.dim, NT) <= 160 * 1024) {
+  if (x3) {
+    // each NSC's small parameters [bn, end of the permuted last bias) as whole
+    // 1 KiB DMA pieces (the blob allocation carries 1 KiB of slack past its end)
+    const int tl = desc.dim / 2 == 1 ? (3 * x3K - 1 + 31) / 32 : zf::x3_last_tiles(x3K);
+    int maxp = 0;
+    for (int i = 0; i < desc.n_ops; ++i) {
+      if (desc.ops[i].kind != ZF_OP_NSC) continue;
+      zf::DevOp& d = F.ops[i];
+      const int64_t end = d.x3_blast + (int64_t)zf::x3_pairs(desc) * tl * 32;
+      d.x3_par_pieces = (int)((end - d.bn) * 4 + 1023) / 1024;
+      maxp = d.x3_par_pieces > maxp ? d.x3_par_pieces : maxp;
+    }
+    F.x3_par_bytes = maxp * 1024;
+  }
+  if (x3 && zf::x3_lds_bytes(zf::x3_buf_tiles(desc, T, x3K), desc.dim + desc.cond_dim, NT, F.x3_par_bytes) <=
+                160 * 1024) {
     zf::x3_pack(desc, nat, T, NT, F, P, x3s);
     F.x3_ok = NT == 3 ? 1 : 2;
     h->x3_K = x3K;
@@ -617,7 +632,8 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   if (e == hipSuccess && use_x3)
     e = hipMemcpy(h->d_x3, x3s.data(), x3s.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&h->d_desc, sizeof(zf::DevFlow));
-  if (e == hipSuccess) e = hipMalloc(&h->d_blob, h->packed.size() * sizeof(float));
+  // + 1 KiB: the split-MFMA kernel DMAs whole 1 KiB pieces of small parameters
+  if (e == hipSuccess) e = hipMalloc(&h->d_blob, h->packed.size() * sizeof(float) + 1024);
   if (e == hipSuccess) e = hipMemcpy(h->d_desc, &h->host, sizeof(zf::DevFlow), hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipMemcpy(h->d_blob, h->packed.data(), h->packed.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -669,9 +685,10 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.desc = h->d_desc; a.blob = h->d_blob; a.x3 = h->d_x3;
     a.x = x; a.c = c; a.y = y; a.ld_in = ld_in; a.ld_out = ld_out; a.lp = lp; a.part = part;
     a.nparts = (N + kBlockRows - 1) / kBlockRows;
-    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.T = h->host.HP / 32;
+    a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.C = h->host.C; a.T = h->host.HP / 32;
     a.NT = h->host.x3_ok == 2 ? 2 : 3;
     a.oact = h->x3_oact;
+    a.par_bytes = h->host.x3_par_bytes;
     a.seed = seed;
     a.gen = gen;
     a.stream = (hipStream_t)stream;

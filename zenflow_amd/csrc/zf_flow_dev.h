@@ -37,12 +37,18 @@ struct DevOp {
   int x3_groups, x3_tlast;
   int x3_next[2];
   int x3_kw[17];  // f16x2: power-of-two weight scale of streamed layer l (1..n_hidden)
+  // split-MFMA kernel: this NSC's small parameters (BatchNorm, Dense_0,
+  // biases, the permuted last bias) are the contiguous blob floats
+  // [bn, bn + 256 * x3_par_pieces), DMA'd into LDS one NSC ahead
+  int x3_par_pieces;
 };
 
 struct DevFlow {
   int D, C, latent, n_ops;
   int HP, nslot, per_wave, x3_ok;
-  int small_floats, _pad[3];  // packed blob [0, small_floats): per-op small parameters
+  int small_floats;  // packed blob [0, small_floats): per-op small parameters
+  int x3_par_bytes;  // split-MFMA kernel: LDS bytes of one NSC's small-parameter region (max over NSCs)
+  int _pad[2];
   float lat_c0, lat_c1, lat_c2, lat_c3;
   DevOp ops[kMaxOps];
 };
@@ -325,9 +331,10 @@ struct X3Launch {
   long long N;
   unsigned long long seed;
   int gen;  // 1: draw the input rows from the latent (zf_flow_sample)
-  int K, D, T;  // knots, dim, hidden tiles (4: width <= 128, 8: <= 256)
+  int K, D, C, T;  // knots, dim, conditions, hidden tiles (4: width <= 128, 8: <= 256)
   int NT;       // split scheme: 3 = bf16x3, 2 = f16x2
   bool oact;    // some coupling's activation is not swish (f16x2 kernels with act switch)
+  int par_bytes;  // DevFlow::x3_par_bytes
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);
@@ -335,7 +342,7 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
 int x3_pairs(const zf_flow_desc& desc);
 int x3_buf_tiles(const zf_flow_desc& desc, int T, int K);
-size_t x3_lds_bytes(int TB, int D, int NT);
+size_t x3_lds_bytes(int TB, int D, int NT, int par_bytes);
 int x3_scheme();
 void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);

@@ -190,9 +190,11 @@ int x3_buf_tiles(const zf_flow_desc& desc, int T, int K) {
   return T > TL ? T : TL;
 }
 
-// TB = x3_buf_tiles
-size_t x3_lds_bytes(int TB, int D, int NT) {
-  return (size_t)2 * 2 * TB * NT * 1024 + (size_t)kX3Waves * 32 * D * 4 + kX3Waves * sizeof(double);
+// TB = x3_buf_tiles; D = dim + cond_dim (the per-wave state holds x and c);
+// par_bytes = DevFlow::x3_par_bytes
+size_t x3_lds_bytes(int TB, int D, int NT, int par_bytes) {
+  return (size_t)2 * 2 * TB * NT * 1024 + (size_t)2 * par_bytes + (size_t)kX3Waves * 32 * D * 4 +
+         kX3Waves * sizeof(double);
 }
 
 int launch_flow_x3(const X3Launch& a, bool inverse) {

@@ -389,6 +389,11 @@ struct X3Pipe {
   int g;        // index of that group within the current NSC
   X3Span span;  // current NSC's group stream
   int wave;
+  // the next NSC's small parameters (DMA'd at step 0 of this NSC into the
+  // other LDS parameter region; null at the last NSC of the range)
+  const char* par_src;
+  char* par_dst;
+  int par_pieces;
 #ifdef ZF_X3_TRACE
   unsigned long long tbar;  // ticks spent in the per-group DMA wait + barrier
 #endif
@@ -399,6 +404,7 @@ struct X3Pipe {
 template <int NT, int T>
 __device__ __forceinline__ void x3_issue_next(const char* __restrict__ x3, const X3Pipe& p, char* dst, int lane) {
   constexpr int kHid = group_bytes<NT>(T);
+  if (p.g == 0 && p.par_src != nullptr) x3_dma(p.par_src, p.par_dst, p.par_pieces, p.wave, lane);
   const int g = p.g + 1;
 #if ZF_X3_ABL == 6  // tuning ablation 6: the stream stops after each NSC's first two groups (real weights stay; wrong results)
   if (g > 1 && g < p.span.G) return;
@@ -632,6 +638,38 @@ __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p,
   }
 }
 
+// Conditioner input + first Dense (bijectors.py:341-343) as zf_flow_dev.h's
+// layer0, with this NSC's small parameters from its LDS region `par` (offsets
+// relative to op.bn) and the conditions from the per-wave state (columns D..)
+// — no global load on the per-coupling path, so no vmcnt wait there drains
+// the weight-group DMA in flight.
+template <int T>
+__device__ __forceinline__ void x3_layer0(const DevOp& op, const float* par, const float* xs, int rot, int D,
+                                          int s, int hh, int lane, floatx16 (&hb)[T], int swish_tiles) {
+  const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
+  const int DCp = 2 * KS0;
+  const float* bn = par;
+  const float* w0b = par + (op.w[0] - op.bn);
+  const float* b0 = par + (op.b[0] - op.bn);
+#pragma unroll
+  for (int o = 0; o < T; ++o) hb[o] = bias_acc(b0 + o * 32, hh);
+  for (int ks = 0; ks < KS0; ++ks) {
+    const int k = 2 * ks + hh;
+    float v = 0.f;
+    if (k < dc) v = xs[wrap(dt + k + rot, D) * 32 + s];
+    else if (k < DC) v = xs[(D + k - dc) * 32 + s];
+    const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
+    const float* w0 = w0b + ks * 64 + lane;
+#pragma unroll
+    for (int o = 0; o < T; ++o) hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
+  }
+#pragma unroll
+  for (int o = 0; o < T; ++o)
+    if (o < swish_tiles)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
+}
+
 // Spline arithmetic of the split-MFMA kernel: the spline parameters already differ from the reference's in the last ulp
 // (GEMM summation order), so the per-lane spline uses ~1-ulp hardware forms:
 // squareplus from v_sqrt_f32 (no Newton step), quotients from a refined
@@ -710,14 +748,19 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   // one LDS weight buffer holds a hidden-layer group (T output tiles) or a
   // last-layer group (TL tiles: more than T at K = 32, hidden 128)
   constexpr int kBuf = group_bytes<NT>(T > TL ? T : TL);
-  // LDS: [2][kBuf] weight groups | [NW][D][32] state | [NW] partials
-  float* xs = reinterpret_cast<float*>(lds + 2 * kBuf) + wave * (32 * D);
-  double* s_part = reinterpret_cast<double*>(reinterpret_cast<float*>(lds + 2 * kBuf) + NW * 32 * D);
+  const int PB = F->x3_par_bytes;
+  const int DS = D + C;  // state columns: x (rotated by `rot`), then c
+  // LDS: [2][kBuf] weight groups | [2][PB] small parameters (NSCs alternate) |
+  //      [NW][DS][32] state | [NW] partials
+  char* par_lds = lds + 2 * kBuf;
+  float* xs = reinterpret_cast<float*>(par_lds + 2 * PB) + wave * (32 * DS);
+  double* s_part = reinterpret_cast<double*>(reinterpret_cast<float*>(par_lds + 2 * PB) + NW * 32 * DS);
   const float* sp = blob;
   const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
   const bool valid = row < N;
 
   load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
+  for (int j = hh; j < C; j += 2) xs[(D + j) * 32 + s] = valid ? cin[row * C + j] : 0.f;
   float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
   int rot = 0;
   wave_lds_sync();
@@ -744,15 +787,26 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #else
 #define X3T(k)
 #endif
-  {  // group 0 of the first NSC in execution order goes out now
+  pipe.par_src = nullptr;
+  pipe.par_dst = nullptr;
+  pipe.par_pieces = 0;
+  {  // group 0 and the small parameters of the first NSC in execution order go out now
     int first = -1;
     const int nq = op_end - op_begin;
     for (int q = 0; q < nq; ++q) {
       const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
       if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
     }
-    if (first >= 0) x3_dma(x3 + F->ops[first].x3, pipe.cur, first_pieces<NT, T>(F->ops[first]), wave, lane);
+    if (first >= 0) {
+      const DevOp& fo = F->ops[first];
+      x3_dma(x3 + fo.x3, pipe.cur, first_pieces<NT, T>(fo), wave, lane);
+      x3_dma(reinterpret_cast<const char*>(blob + fo.bn), par_lds, fo.x3_par_pieces, wave, lane);
+    }
+    // its layer 0 reads the parameters before any group step's wait
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
+  int nsc_i = 0;  // NSCs entered, in execution order: parameter region nsc_i & 1
 
   const KnotConsts kc(K);
   const int nq = op_end - op_begin;
@@ -772,6 +826,15 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #endif
       pipe.span = make_span<NT, T, INV>(F, oi, op_begin, op_end);
       pipe.g = 0;
+      const float* par = reinterpret_cast<const float*>(par_lds + (nsc_i & 1) * PB);
+      {
+        const int n = op.x3_next[INV ? 1 : 0];
+        const bool has_next = n >= op_begin && n < op_end;
+        pipe.par_src = has_next ? reinterpret_cast<const char*>(blob + F->ops[n].bn) : nullptr;
+        pipe.par_dst = par_lds + ((nsc_i + 1) & 1) * PB;
+        pipe.par_pieces = has_next ? F->ops[n].x3_par_pieces : 0;
+      }
+      ++nsc_i;
       floatx16 hb[T];
       // The swish of a layer's output is deferred tile by tile into the next
       // streamed layer (x3_step, SW) — except before a PAIRS last layer,
@@ -780,8 +843,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       constexpr bool kPipe = T == 4 && !PAIRS;
       // f16x2: every layer leaves raw pre-activations; the next streamed
       // layer scales and swishes them (act_swish) as it goes.
-      layer0<T>(op, sp, xs, cin, row, valid, C, rot, D, s, hh, lane, hb,
-                NT == 2 ? 0 : (op.n_hidden > 1 || kLastSW) ? 1 : T);
+      x3_layer0<T>(op, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (op.n_hidden > 1 || kLastSW) ? 1 : T);
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
       // biases seed the accumulators.  f16x2: they seed them divided by the
       // unscale (exact: powers of two) and the accumulators are multiplied
@@ -805,11 +867,12 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
           for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT>(hb[o], isc, op.act);
         }
+        const float* bl_l = par + (op.b[l] - op.bn);
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          acc[o] = NT == 3 ? bias_acc(sp + op.b[l] + o * 32, hh)
-                           : (kSeedScaled ? bias_acc(sp + op.b[l] + o * 32, hh) * ius : floatx16{0});
-        const float* bh = (NT == 2 && !kSeedScaled) ? sp + op.b[l] : nullptr;
+          acc[o] = NT == 3 ? bias_acc(bl_l + o * 32, hh)
+                           : (kSeedScaled ? bias_acc(bl_l + o * 32, hh) * ius : floatx16{0});
+        const float* bh = (NT == 2 && !kSeedScaled) ? bl_l : nullptr;
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
@@ -854,7 +917,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         // live across pairs anyway; otherwise it joins in the last step, when
         // the first input tiles are dead (fewer registers at the peak);
         // f16x2 always joins it at the end, with the unscale.
-        const float* bl = sp + op.x3_blast + pr * TL * 32;
+        const float* bl = par + (op.x3_blast - op.bn) + pr * TL * 32;
         floatx16 pa[TL];
         constexpr bool kSeed = PAIRS && NT == 3;
 #pragma unroll
@@ -963,8 +1026,8 @@ int launch_x3(const X3Launch& a, bool inverse) {
   const long long grid = (a.N + rows - 1) / rows;
   if (grid > 0x7fffffffLL) return einval("N too large");
   constexpr int TL = ONE ? (3 * K - 1 + 31) / 32 : (3 * K - 1 + 15) / 16;
-  size_t lds = (size_t)2 * group_bytes<NT>(T > TL ? T : TL) + (size_t)kX3Waves * 32 * a.D * 4 +
-               kX3Waves * sizeof(double);
+  size_t lds = (size_t)2 * group_bytes<NT>(T > TL ? T : TL) + (size_t)2 * a.par_bytes +
+               (size_t)kX3Waves * 32 * (a.D + a.C) * 4 + kX3Waves * sizeof(double);
 #ifdef ZF_X3_TRACE
   if (const char* pad = std::getenv("ZF_X3_LDS_PAD")) lds += (size_t)std::atoi(pad) * 1024;  // occupancy probe
 #endif
