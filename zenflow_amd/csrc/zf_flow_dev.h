@@ -41,6 +41,11 @@ struct DevOp {
   // biases, the permuted last bias) are the contiguous blob floats
   // [bn, bn + 256 * x3_par_pieces), DMA'd into LDS one NSC ahead
   int x3_par_pieces;
+  // the next NSC in forward / inverse execution order (x3_next[d] >= 0):
+  // its group-0 byte offset and pieces, its parameter block and pieces —
+  // copied here so the kernel's per-NSC scalars are one batch of independent loads
+  long long x3_nbase[2], x3_nbn[2];
+  int x3_npieces[2], x3_npar[2];
 };
 
 struct DevFlow {

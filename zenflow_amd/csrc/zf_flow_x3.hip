@@ -171,6 +171,8 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
       for (int l = 0; l < op.n_hidden; ++l)
         for (int64_t i = 0; i < (int64_t)T * 32; ++i) packed[d.b[l] + i] *= kSwishPrescale;
     }
+    // group-0 pieces of this NSC (hidden group, or a last-layer group when it has no hidden streamed layer)
+    d.x3_npieces[0] = d.x3_npieces[1] = (2 * (op.n_hidden > 1 ? T : TL) * NT * 1024) >> 10;  // own; fixed below
     // permuted last bias: [pair][o][lane half h][r] = bias[(2 pair + h) S + 16o + r]
     const float* B = nat + op.off_b[op.n_hidden];
     for (int pr = 0; pr < NP; ++pr)
@@ -180,6 +182,20 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
             const int jp = one ? 32 * o + 16 * h + r : 16 * o + r, dd = one ? 0 : 2 * pr + h;
             packed[d.x3_blast + ((pr * TL + o) * 2 + h) * 16 + r] = (dd < dt && jp < S) ? B[dd * S + jp] : 0.f;
           }
+  }
+  // next-NSC copies (x3_npieces above held each op's own group-0 pieces)
+  std::vector<int> own(desc.n_ops, 0);
+  for (int i = 0; i < desc.n_ops; ++i) own[i] = desc.ops[i].kind == ZF_OP_NSC ? F.ops[i].x3_npieces[0] : 0;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    if (desc.ops[i].kind != ZF_OP_NSC) continue;
+    DevOp& d = F.ops[i];
+    for (int dir = 0; dir < 2; ++dir) {
+      const int n = d.x3_next[dir];
+      d.x3_nbase[dir] = n >= 0 ? F.ops[n].x3 : -1;
+      d.x3_nbn[dir] = n >= 0 ? F.ops[n].bn : 0;
+      d.x3_npieces[dir] = n >= 0 ? own[n] : 0;
+      d.x3_npar[dir] = n >= 0 ? F.ops[n].x3_par_pieces : 0;
+    }
   }
 }
 

@@ -351,22 +351,40 @@ __device__ __forceinline__ int first_pieces(const DevOp& op) {
   return (op.n_hidden > 1 ? group_bytes<NT>(T) : group_bytes<NT>(op.x3_tlast)) >> 10;
 }
 
-template <int NT, int T, bool INV>
-__device__ __forceinline__ X3Span make_span(const DevFlow* __restrict__ F, int oi, int op_begin, int op_end) {
-  const DevOp& op = F->ops[oi];
+// Every scalar of one op the kernel uses, read at the top of the op loop for
+// every op kind: one batch of independent scalar loads and one wait, instead
+// of a chain of load -> wait -> branch -> load (each lgkmcnt(0) wait there
+// also drains the wave's outstanding LDS reads).
+struct X3Sc {
+  int kind, shift, nh, act, dt, dc, DC, KS0, G, tlast, nxt, npieces, npar, kw1, kw_last;
+  long long x3, nbase, nbn, bn, w0_rel, b_rel, blast_rel, sb;
+};
+
+template <bool INV>
+__device__ __forceinline__ X3Sc x3_scalars(const DevOp& op) {
+  constexpr int d = INV ? 1 : 0;
+  X3Sc c;
+  c.kind = op.kind; c.shift = op.shift; c.nh = op.n_hidden; c.act = op.act;
+  c.dt = op.dt; c.dc = op.dc; c.DC = op.DC; c.KS0 = op.KS0;
+  c.G = op.x3_groups; c.tlast = op.x3_tlast; c.nxt = op.x3_next[d];
+  c.npieces = op.x3_npieces[d]; c.npar = op.x3_npar[d];
+  c.kw1 = op.x3_kw[1];
+  c.kw_last = op.x3_kw[op.n_hidden & 15];
+  c.x3 = op.x3; c.nbase = op.x3_nbase[d]; c.nbn = op.x3_nbn[d]; c.bn = op.bn;
+  c.w0_rel = op.w[0] - op.bn; c.b_rel = op.b[0] - op.bn; c.blast_rel = op.x3_blast - op.bn;
+  c.sb = op.sb;
+  return c;
+}
+
+template <int NT, int T>
+__device__ __forceinline__ X3Span make_span(const X3Sc& c, bool has_next) {
   X3Span sp;
-  sp.base = op.x3;
-  sp.G = op.x3_groups;
-  sp.nhid = T * (op.n_hidden - 1);
-  sp.last_pieces = group_bytes<NT>(op.x3_tlast) >> 10;
-  const int n = op.x3_next[INV ? 1 : 0];
-  if (n >= op_begin && n < op_end) {
-    sp.next_base = F->ops[n].x3;
-    sp.next_pieces = first_pieces<NT, T>(F->ops[n]);
-  } else {
-    sp.next_base = -1;
-    sp.next_pieces = 0;
-  }
+  sp.base = c.x3;
+  sp.G = c.G;
+  sp.nhid = T * (c.nh - 1);
+  sp.last_pieces = group_bytes<NT>(c.tlast) >> 10;
+  sp.next_base = has_next ? c.nbase : -1;
+  sp.next_pieces = has_next ? c.npieces : 0;
   return sp;
 }
 
@@ -644,13 +662,13 @@ __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p,
 // — no global load on the per-coupling path, so no vmcnt wait there drains
 // the weight-group DMA in flight.
 template <int T>
-__device__ __forceinline__ void x3_layer0(const DevOp& op, const float* par, const float* xs, int rot, int D,
+__device__ __forceinline__ void x3_layer0(const X3Sc& c, const float* par, const float* xs, int rot, int D,
                                           int s, int hh, int lane, floatx16 (&hb)[T], int swish_tiles) {
-  const int dt = op.dt, dc = op.dc, DC = op.DC, KS0 = op.KS0;
+  const int dt = c.dt, dc = c.dc, DC = c.DC, KS0 = c.KS0;
   const int DCp = 2 * KS0;
   const float* bn = par;
-  const float* w0b = par + (op.w[0] - op.bn);
-  const float* b0 = par + (op.b[0] - op.bn);
+  const float* w0b = par + c.w0_rel;
+  const float* b0 = par + c.b_rel;
 #pragma unroll
   for (int o = 0; o < T; ++o) hb[o] = bias_acc(b0 + o * 32, hh);
   for (int ks = 0; ks < KS0; ++ks) {
@@ -813,28 +831,31 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   for (int q = 0; q < nq; ++q) {
     const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
     const DevOp& op = F->ops[oi];
-    const int kind = op.kind;
+    const X3Sc opc = x3_scalars<INV>(op);
+    const int kind = opc.kind;
     if (kind == ZF_OP_ROLL) {  // bijectors.py:291 / :296
-      rot = pmod(INV ? rot + op.shift : rot - op.shift, D);
+      rot = pmod(INV ? rot + opc.shift : rot - opc.shift, D);
     } else if (kind == ZF_OP_SHIFT_BOUNDS) {
-      shift_bounds_op<INV>(sp + op.sb, xs, s, hh, rot, D, ld);
+      shift_bounds_op<INV>(sp + opc.sb, xs, s, hh, rot, D, ld);
       X3T(10);
     } else {  // ZF_OP_NSC, bijectors.py:329-371
       X3T(0);
 #ifdef ZF_X3_TRACE
       tacc[9] += 1;
 #endif
-      pipe.span = make_span<NT, T, INV>(F, oi, op_begin, op_end);
+      {  // the next NSC's stream and parameters from this op's own record
+        const bool has_next = opc.nxt >= op_begin && opc.nxt < op_end;
+        pipe.span = make_span<NT, T>(opc, has_next);
+        pipe.par_src = has_next ? reinterpret_cast<const char*>(blob + opc.nbn) : nullptr;
+        pipe.par_dst = par_lds + ((nsc_i + 1) & 1) * PB;
+        pipe.par_pieces = has_next ? opc.npar : 0;
+      }
       pipe.g = 0;
       const float* par = reinterpret_cast<const float*>(par_lds + (nsc_i & 1) * PB);
-      {
-        const int n = op.x3_next[INV ? 1 : 0];
-        const bool has_next = n >= op_begin && n < op_end;
-        pipe.par_src = has_next ? reinterpret_cast<const char*>(blob + F->ops[n].bn) : nullptr;
-        pipe.par_dst = par_lds + ((nsc_i + 1) & 1) * PB;
-        pipe.par_pieces = has_next ? F->ops[n].x3_par_pieces : 0;
-      }
       ++nsc_i;
+      const int nh = opc.nh, act = opc.act, dt = opc.dt, kw_last = opc.kw_last;
+      // hidden biases are consecutive T x 32 blocks after Dense_0's (zf_flow.hip: b[l] = b[0] + l T 32)
+      const long long b_rel = opc.b_rel + T * 32, blast_rel = opc.blast_rel;
       floatx16 hb[T];
       // The swish of a layer's output is deferred tile by tile into the next
       // streamed layer (x3_step, SW) — except before a PAIRS last layer,
@@ -843,7 +864,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       constexpr bool kPipe = T == 4 && !PAIRS;
       // f16x2: every layer leaves raw pre-activations; the next streamed
       // layer scales and swishes them (act_swish) as it goes.
-      x3_layer0<T>(op, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (op.n_hidden > 1 || kLastSW) ? 1 : T);
+      x3_layer0<T>(opc, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (nh > 1 || kLastSW) ? 1 : T);
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
       // biases seed the accumulators.  f16x2: they seed them divided by the
       // unscale (exact: powers of two) and the accumulators are multiplied
@@ -857,17 +878,17 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       if constexpr (T == 4) __builtin_amdgcn_s_setprio(2);
 #endif
       X3T(1);
-      for (int l = 1; l < op.n_hidden; ++l) {
+      for (int l = 1; l < nh; ++l) {
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;
         if constexpr (NT == 2) {
-          x3_act_scale<T, OACT>(hb, op.x3_kw[l], isc, us, ius, op.act);
+          x3_act_scale<T, OACT>(hb, l == 1 ? opc.kw1 : op.x3_kw[l], isc, us, ius, act);
           // OACT: every tile here, outside the MFMA stream (the switch there
           // would cost a third of the waves)
 #pragma unroll
-          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT>(hb[o], isc, op.act);
+          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT>(hb[o], isc, act);
         }
-        const float* bl_l = par + (op.b[l] - op.bn);
+        const float* bl_l = par + b_rel + (l - 1) * (T * 32);
 #pragma unroll
         for (int o = 0; o < T; ++o)
           acc[o] = NT == 3 ? bias_acc(bl_l + o * 32, hh)
@@ -877,15 +898,15 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
           x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
-                                                                 op.act);
+                                                                 act);
         } else {
-          x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, op.act);
+          x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, act);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
           for (int o = 0; o < T; ++o) acc[o] *= us;
         }
-        const int nsw = NT == 2 ? 0 : (l + 1 < op.n_hidden || kLastSW) ? 1 : T;
+        const int nsw = NT == 2 ? 0 : (l + 1 < nh || kLastSW) ? 1 : T;
 #pragma unroll
         for (int o = 0; o < T; ++o) {
           if (o < nsw) {
@@ -899,25 +920,24 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       X3T(2);
       // Last Dense (:346-347), one pair of transformed dims at a time: lane
       // half h, tile o, register r = parameter 16*o + r of dim 2*pair + h.
-      const int dt = op.dt;
       float ldn = 0.f;  // this coupling's log-det, summed in dim order (utils.py:139)
       // PAIRS == false: one pair (dt <= 2), and the hidden activations are
       // dead once the last layer has consumed them.
       const int npair = PAIRS ? (dt + 1) / 2 : 1;
       float lisc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
       if constexpr (NT == 2) {
-        x3_act_scale<T, OACT>(hb, op.x3_kw[op.n_hidden], lisc, lus, lius, op.act);
+        x3_act_scale<T, OACT>(hb, kw_last, lisc, lus, lius, act);
         // PAIRS: the input is read once per dim pair, so swish it whole here
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT>(hb[o], lisc, op.act);
+          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT>(hb[o], lisc, act);
       }
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
         // live across pairs anyway; otherwise it joins in the last step, when
         // the first input tiles are dead (fewer registers at the peak);
         // f16x2 always joins it at the end, with the unscale.
-        const float* bl = par + (op.x3_blast - op.bn) + pr * TL * 32;
+        const float* bl = par + blast_rel + pr * TL * 32;
         floatx16 pa[TL];
         constexpr bool kSeed = PAIRS && NT == 3;
 #pragma unroll
@@ -927,10 +947,10 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
-          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, op.act);
+          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, act);
         } else {
           x3_layer<NT, T, TL, kLastSW, OACT>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh,
-                                             lisc, lus, op.act);
+                                             lisc, lus, act);
         }
         if constexpr (kSeedScaled) {
 #pragma unroll
@@ -953,7 +973,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           }
         // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
         const int d = 2 * pr + hh;
-        const bool act = d < dt;  // the upper half idles on an odd last dim
+        const bool dact = d < dt;  // the upper half idles on an odd last dim
         float ldv = 0.f;
         {
           float w[K], hg[K];
@@ -979,7 +999,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
           for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
-          float* xp = xs + wrap((act ? d : 0) + rot, D) * 32 + s;
+          float* xp = xs + wrap((dact ? d : 0) + rot, D) * 32 + s;
           const float xv = *xp;
           const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
                                                        [](float v) { return v == 0.f ? 1.f : x3_squareplus(v); });
@@ -987,11 +1007,11 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           if (!INV) {
             float l;
             x3_forward_eval(xv, bin, yv, l);
-            ldv = act ? l : 0.f;
+            ldv = dact ? l : 0.f;
           } else {
             yv = rqs_inverse_eval(xv, bin);
           }
-          if (act) *xp = yv;
+          if (dact) *xp = yv;
         }
         wave_lds_sync();
         if (!INV) {
