@@ -562,6 +562,23 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
   }
+#if defined(ZF_X3_EXP) && ZF_X3_EXP == 3
+  // experimental: each (k-step, tile) triple as [2 fragment reads][VALU x5]
+  // [MFMA][VALU x3][MFMA][VALU x3][MFMA], so the step's VALU issues between
+  // the dependent MFMAs of a triple instead of after it
+  {
+#pragma unroll
+    for (int i = 0; i < 2 * NOUT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+#pragma unroll
+      for (int m = 0; m < XT<NT>::kProd; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (m + 1 < XT<NT>::kProd) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+    }
+  }
+#endif
   char* const t = p.cur;
   p.cur = p.nxt;
   p.nxt = t;
@@ -624,16 +641,95 @@ __device__ __forceinline__ void x3_step_up(const char* __restrict__ x3, X3Pipe& 
 }
 #endif
 
+// One product term of a (k-step, tile) triple: j = 0: lo*hi, 1: hi*lo, 2: hi*hi
+// (f16x2, small terms first as mfma_split).
+__device__ __forceinline__ floatx16 mfma_term2(const halfx8 (&a)[2], const halfx8 (&b)[2], int j, floatx16 acc) {
+  if (j == 0) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], acc, 0, 0, 0);
+  if (j == 1) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// f16x2, hidden 128, swish: the step as 2 x NOUT x 3 MFMA slots in a fixed
+// order, each slot = one MFMA + its share of the step's VALU (the split of
+// k-step (Q, 1), the swish of tile Q+1 one value per slot, the split of
+// (Q+1, 0)), pinned by scheduling barriers, so the VALU issues between the
+// MFMAs of the wave's own dependent triples instead of after them; the A
+// fragments of the next triple are read one triple ahead.
+template <int T, int NOUT, int Q, bool HASB>
+__device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                              int hh, halfx8 (&cs)[2], float isc, float us) {
+  constexpr int NT = 2;
+#ifdef ZF_X3_TRACE
+  const unsigned long long tb0 = X3T_NOW();
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#ifdef ZF_X3_TRACE
+  p.tbar += X3T_NOW() - tb0;
+#endif
+  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+  floatx16 bt[NOUT];
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
+  }
+  const char* lb = p.cur + lane * 16;
+  halfx8 fr[2][NT];
+  load_frag<NT>(lb, fr[0]);
+  halfx8 s1[NT];
+  constexpr int kSlots = 2 * NOUT * 3;
+  // swish values placed in slots 1..kSw, the split of (Q+1, 0) in slot kSplit
+  // (or after the slots when a small group has too few: NOUT = 1, 2)
+  constexpr int kSw = kSlots - 2 < 16 ? kSlots - 2 : 16;
+  constexpr int kSplit = kSw == 16 ? (kSlots - 1 < 18 ? kSlots - 1 : 18) : kSlots;
+#pragma unroll
+  for (int m = 0; m < kSlots; ++m) {
+    const int t = m / 3, j = m % 3, ks = t / NOUT, o = t % NOUT;
+    if (j == 0 && t + 1 < 2 * NOUT) load_frag<NT>(lb + (((t + 1) * NT) << 10), fr[(t + 1) & 1]);
+    acc[o] = mfma_term2(fr[t & 1], ks == 0 ? cs : s1, j, acc[o]);
+    if (m == 0) splitk<NT, 1>(hb[Q], s1);
+    if constexpr (Q + 1 < T) {
+      if (m >= 1 && m <= kSw) hb[Q + 1][m - 1] = act_swish<NT>(hb[Q + 1][m - 1], isc);
+      if (m == kSplit) splitk<NT, 0>(hb[Q + 1], cs);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (Q + 1 < T && kSplit >= kSlots) {
+#pragma unroll
+    for (int r = kSw; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
+    splitk<NT, 0>(hb[Q + 1], cs);
+  }
+  static_assert(kSlots >= 2, "at least one triple per k-step");
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+  }
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
 template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
                                               typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
-#ifdef ZF_X3_EXP
+#if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
 #define X3_STEP x3_step_up
 #else
 #define X3_STEP x3_step_pipe
 #endif
+  if constexpr (NT == 2 && !OACT) {  // the swish kernels: explicit MFMA slots (x3_step_slots)
+    if constexpr (Q + 1 < T) {
+      x3_step_slots<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us);
+      x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
+    } else {
+      x3_step_slots<T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
+    }
+    return;
+  }
   if constexpr (Q + 1 < T) {
     X3_STEP<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
     x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
@@ -739,7 +835,7 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
 // all tiles before the layer's groups instead of tile by tile inside them
 // (a switch inside the pipelined steps spilled 110-130 VGPRs at 3 waves).
 template <int T, int K, bool PAIRS>
-#ifdef ZF_X3_EXP
+#if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
 constexpr int x3_occupancy() { return T == 8 ? 1 : 2; }
 #else
 constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
