@@ -41,6 +41,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 namespace zf {
@@ -139,6 +140,37 @@ __device__ __forceinline__ void split8h(const floatx16& v, halfx8& bh, halfx8& b
   }
   asm(
       "v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, 1.0, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, 1.0, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, 1.0, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, 1.0, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(l[0]), "=&v"(l[1]), "=&v"(l[2]), "=&v"(l[3])
+      : "v"(v[8 * S + 0]), "v"(v[8 * S + 1]), "v"(v[8 * S + 2]), "v"(v[8 * S + 3]), "v"(v[8 * S + 4]),
+        "v"(v[8 * S + 5]), "v"(v[8 * S + 6]), "v"(v[8 * S + 7]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
+  __builtin_memcpy(&bh, h, 16);
+  __builtin_memcpy(&bl, l, 16);
+}
+
+// split8h in two halves for the slot schedule: the hi terms (4 v_cvt_pk),
+// then the lo terms (the asm block, one slot later, so it does not wait on
+// the conversions' latency).
+template <int S>
+__device__ __forceinline__ void split8h_hi(const floatx16& v, uint32_t (&h)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const halfx2 hv = __builtin_convertvector(floatx2{v[8 * S + 2 * i], v[8 * S + 2 * i + 1]}, halfx2);
+    __builtin_memcpy(&h[i], &hv, 4);
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void split8h_lo(const floatx16& v, const uint32_t (&h)[4], halfx8& bh, halfx8& bl) {
+  uint32_t l[4];
+  asm("v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
       "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
       "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
       "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
@@ -649,6 +681,67 @@ __device__ __forceinline__ floatx16 mfma_term2(const halfx8 (&a)[2], const halfx
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
 }
 
+// VALU work items of slot m of x3_step_slots (a slot's items are independent
+// of each other, so none waits on another's latency inside the slot):
+//   slot 0: hi terms of the split of (Q, 1); slot 1: its lo terms;
+//   swish of tile Q+1 as a 4-stage modulo pipeline, value i: exp at slot
+//   i+1, fma at i+2, rcp at i+3, mul at i+4 (ring of 4 temporaries);
+//   split of (Q+1, 0) (needs values 0..7, whose muls end at slot 11): hi at
+//   slot max(12, 3 NOUT), lo one slot later — after the k-step-0 MFMAs that read cs.
+// Slots past the group's last MFMA run after it, in the same order.
+template <int T, int NOUT, int Q, int m>
+__device__ __forceinline__ void x3_valu_slot(floatx16 (&hb)[T], halfx8 (&cs)[2], halfx8 (&s1)[2], float (&tq)[4],
+                                             uint32_t (&s1h)[4], uint32_t (&csh)[4], float c) {
+  // the split of (Q+1, 0) overwrites cs: not before the last k-step-0 MFMA (slot 3 NOUT - 1)
+  constexpr int kCs = 3 * NOUT > 12 ? 3 * NOUT : 12;
+  if constexpr (m == 0) split8h_hi<1>(hb[Q], s1h);
+  if constexpr (m == 1) split8h_lo<1>(hb[Q], s1h, s1[0], s1[1]);
+  if constexpr (Q + 1 < T) {
+    constexpr int i0 = m - 1, i1 = m - 2, i2 = m - 3, i3 = m - 4;
+    if constexpr (i3 >= 0 && i3 < 16) {
+      hb[Q + 1][i3] = hb[Q + 1][i3] * tq[i3 & 3];
+      // pin the value here: values 8..15 are only read by the next group's
+      // split, and machine sinking would otherwise move their whole chain there
+      asm volatile("" ::"v"(hb[Q + 1][i3]));
+    }
+    if constexpr (i2 >= 0 && i2 < 16) tq[i2 & 3] = __builtin_amdgcn_rcpf(tq[i2 & 3]);
+    if constexpr (i1 >= 0 && i1 < 16) tq[i1 & 3] = __builtin_fmaf(tq[i1 & 3], c, c);
+    if constexpr (i0 >= 0 && i0 < 16) tq[i0 & 3] = __builtin_amdgcn_exp2f(-hb[Q + 1][i0]);
+    if constexpr (m == kCs) split8h_hi<0>(hb[Q + 1], csh);
+    if constexpr (m == kCs + 1) split8h_lo<0>(hb[Q + 1], csh, cs[0], cs[1]);
+  }
+}
+
+// Slot m: one MFMA term of triple m / 3 (the next triple's A fragments read
+// at its first term), then the slot's VALU, then a scheduling barrier that
+// keeps the compiler from regrouping the MFMAs.
+template <int T, int NOUT, int Q, int m>
+__device__ __forceinline__ void x3_slot(const char* lb, floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
+                                        halfx8 (&fr)[2][2], halfx8 (&cs)[2], halfx8 (&s1)[2], float (&tq)[4],
+                                        uint32_t (&s1h)[4], uint32_t (&csh)[4], float c) {
+  constexpr int t = m / 3, j = m % 3, ks = t / NOUT, o = t % NOUT;
+  if constexpr (j == 0 && t + 1 < 2 * NOUT) load_frag<2>(lb + (((t + 1) * 2) << 10), fr[(t + 1) & 1]);
+  if constexpr (ks == 0) acc[o] = mfma_term2(fr[t & 1], cs, j, acc[o]);
+  else acc[o] = mfma_term2(fr[t & 1], s1, j, acc[o]);
+  x3_valu_slot<T, NOUT, Q, m>(hb, cs, s1, tq, s1h, csh, c);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int T, int NOUT, int Q, int... M>
+__device__ __forceinline__ void x3_slots_all(std::integer_sequence<int, M...>, const char* lb, floatx16 (&hb)[T],
+                                             floatx16 (&acc)[NOUT], halfx8 (&fr)[2][2], halfx8 (&cs)[2],
+                                             halfx8 (&s1)[2], float (&tq)[4], uint32_t (&s1h)[4],
+                                             uint32_t (&csh)[4], float c) {
+  (x3_slot<T, NOUT, Q, M>(lb, hb, acc, fr, cs, s1, tq, s1h, csh, c), ...);
+}
+
+template <int T, int NOUT, int Q, int... M>
+__device__ __forceinline__ void x3_valu_tail(std::integer_sequence<int, M...>, floatx16 (&hb)[T], halfx8 (&cs)[2],
+                                             halfx8 (&s1)[2], float (&tq)[4], uint32_t (&s1h)[4],
+                                             uint32_t (&csh)[4], float c) {
+  (x3_valu_slot<T, NOUT, Q, 2 * NOUT * 3 + M>(hb, cs, s1, tq, s1h, csh, c), ...);
+}
+
 // f16x2, hidden 128, swish: the step as 2 x NOUT x 3 MFMA slots in a fixed
 // order, each slot = one MFMA + its share of the step's VALU (the split of
 // k-step (Q, 1), the swish of tile Q+1 one value per slot, the split of
@@ -679,27 +772,20 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
   load_frag<NT>(lb, fr[0]);
   halfx8 s1[NT];
   constexpr int kSlots = 2 * NOUT * 3;
-  // swish values placed in slots 1..kSw, the split of (Q+1, 0) in slot kSplit
-  // (or after the slots when a small group has too few: NOUT = 1, 2)
-  constexpr int kSw = kSlots - 2 < 16 ? kSlots - 2 : 16;
-  constexpr int kSplit = kSw == 16 ? (kSlots - 1 < 18 ? kSlots - 1 : 18) : kSlots;
-#pragma unroll
-  for (int m = 0; m < kSlots; ++m) {
-    const int t = m / 3, j = m % 3, ks = t / NOUT, o = t % NOUT;
-    if (j == 0 && t + 1 < 2 * NOUT) load_frag<NT>(lb + (((t + 1) * NT) << 10), fr[(t + 1) & 1]);
-    acc[o] = mfma_term2(fr[t & 1], ks == 0 ? cs : s1, j, acc[o]);
-    if (m == 0) splitk<NT, 1>(hb[Q], s1);
-    if constexpr (Q + 1 < T) {
-      if (m >= 1 && m <= kSw) hb[Q + 1][m - 1] = act_swish<NT>(hb[Q + 1][m - 1], isc);
-      if (m == kSplit) splitk<NT, 0>(hb[Q + 1], cs);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (Q + 1 < T && kSplit >= kSlots) {
-#pragma unroll
-    for (int r = kSw; r < 16; ++r) hb[Q + 1][r] = act_swish<NT>(hb[Q + 1][r], isc);
-    splitk<NT, 0>(hb[Q + 1], cs);
-  }
+  // VALU work items by slot (a slot's items are independent of each other,
+  // so none waits on another's latency inside the slot):
+  //   slot 0: hi terms of the split of (Q, 1); slot 1: its lo terms;
+  //   swish of tile Q+1 as a 4-stage modulo pipeline, value i: exp at slot
+  //   i+1, fma at i+2, rcp at i+3, mul at i+4 (ring of 4 temporaries);
+  //   split of (Q+1, 0) (needs values 0..7: their muls end at slot 11):
+  //   hi at slot 12, lo at slot 13 — after the k-step-0 MFMAs that read cs.
+  // Stages that fall past the last slot run after it, in the same order.
+  float tq[4];
+  uint32_t s1h[4], csh[4];
+  x3_slots_all<T, NOUT, Q>(std::make_integer_sequence<int, kSlots>{}, lb, hb, acc, fr, cs, s1, tq, s1h, csh, isc);
+  // the stages that did not fit in the slots (small groups), in slot order
+  x3_valu_tail<T, NOUT, Q>(std::make_integer_sequence<int, (kSlots < 20 ? 20 - kSlots : 0)>{}, hb, cs, s1, tq,
+                           s1h, csh, isc);
   static_assert(kSlots >= 2, "at least one triple per k-step");
   if constexpr (HASB) {
 #pragma unroll
