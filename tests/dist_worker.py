@@ -85,16 +85,19 @@ def main(mode, outdir):
         _train_dp(rdzv, res, outdir)
     elif mode == "train_fn":
         _train_fn(rdzv, res, outdir)
+    elif mode == "train_rccl":
+        _train_dp(rdzv, res, outdir, rccl=True)
     rdzv.close()
     Path(outdir, f"rank{rank}.json").write_text(json.dumps(res))
 
 
-def _train_dp(rdzv, res, outdir):
-    """One rank of data-parallel training on a shared GPU (HostAllgather):
-    loss_grad on this rank's shard, then ZF_TEST_STEPS optimiser steps;
-    the gradient, loss and final blob go to <outdir>/rank<r>.npz."""
+def _train_dp(rdzv, res, outdir, rccl=False):
+    """One rank of data-parallel training: loss_grad on this rank's shard,
+    then ZF_TEST_STEPS optimiser steps; the gradient, loss and final blob go
+    to <outdir>/rank<r>.npz.  Ranks share one GPU through HostAllgather, or
+    (``rccl``) each rank drives its own GPU (LOCAL_RANK) over RCCL."""
     from tests.flowcases import build_flow, make_case
-    from zenflow_amd.dist import HostAllgather, shard_rows
+    from zenflow_amd.dist import HostAllgather, RcclCommunicator, shard_rows
     from zenflow_amd.train import Trainer
 
     name, N, seed = os.environ["ZF_TEST_CASE"].split(":")
@@ -104,7 +107,10 @@ def _train_dp(rdzv, res, outdir):
     cfg = case["cfg"]
     flow = build_flow(cfg)
     flow.latent._dim = cfg["D"]
-    comm = HostAllgather(rdzv)
+    if rccl:
+        comm = RcclCommunicator(rdzv.rank, rdzv.world, lambda u: rdzv.broadcast_bytes(u, tag="rccl_uid"))
+    else:
+        comm = HostAllgather(rdzv)
     a, b = shard_rows(N, rdzv.rank, rdzv.world)
     x = case["x"][a:b]
     c = None if case["c"] is None else case["c"][a:b]
@@ -119,7 +125,8 @@ def _train_dp(rdzv, res, outdir):
     np.savez(Path(outdir, f"rank{rdzv.rank}.npz"), grad=g, loss=np.float64(loss), blob=blob,
              last_loss=np.float64(tr.last_loss()))
     res["rows"] = b - a
-
+    if rccl:
+        comm.close()
 
 
 def two_moons_flow():
@@ -145,7 +152,8 @@ def _train_fn(rdzv, res, outdir):
     from zenflow_amd.io import flatten_variables
 
     X = two_moons_data()
-    best, best_epoch, lt, ls = zf.train(two_moons_flow(), X[:2400], X[2400:], epochs=int(os.environ.get("ZF_TEST_EPOCHS", "20")),
+    n = int(os.environ.get("ZF_TEST_NTRAIN", "2400"))
+    best, best_epoch, lt, ls = zf.train(two_moons_flow(), X[:n], X[2400:], epochs=int(os.environ.get("ZF_TEST_EPOCHS", "20")),
                                         batch_size=512, progress=False, comm=HostAllgather(rdzv))
     np.savez(Path(outdir, f"rank{rdzv.rank}.npz"), best_epoch=best_epoch, lt=np.asarray(lt), ls=np.asarray(ls),
              **{"v:" + k: v for k, v in flatten_variables(best).items()})

@@ -142,6 +142,21 @@ class Trainer:
         check(L.load_library().zf_trainer_step_shard(self.handle, xptr, cptr, rows, self._global(rows, global_rows),
                                                      self._loss.ptr, L.stream()), "zf_trainer_step")
 
+    def _step_local(self, xptr: int, cptr: Optional[int], rows: int) -> None:
+        """One step on the whole batch without the cross-rank reductions:
+        every rank holds the same batch, so each computes the one-device
+        step itself (a batch with fewer rows than ranks)."""
+        lib = L.load_library()
+        if self.world > 1:
+            check(lib.zf_trainer_set_comm(self.handle, None), "zf_trainer_set_comm")
+        try:
+            self._last_rows = rows
+            check(lib.zf_trainer_step_shard(self.handle, xptr, cptr, rows, rows, self._loss.ptr, L.stream()),
+                  "zf_trainer_step")
+        finally:
+            if self.world > 1:
+                check(lib.zf_trainer_set_comm(self.handle, ct.byref(self._comm_desc)), "zf_trainer_set_comm")
+
     def last_loss(self) -> float:
         return self._fp32_mean(float(self._loss.numpy()[0]))
 
@@ -198,8 +213,10 @@ def train(
     ``comm`` (data parallelism, one process per GPU, every rank calling with
     the same data and seed): each global batch of ``batch_size`` rows is cut
     into contiguous per-rank shards (``dist.shard_rows``); the trainer's
-    reductions make every rank's parameters identical after every step.  A
-    batch with fewer rows than ranks is skipped."""
+    reductions make every rank's parameters identical after every step, and
+    equal to one device's when every batch splits evenly.  A batch with fewer
+    rows than ranks is stepped by every rank on the whole batch, without
+    reductions (the one-device step)."""
     if warmup < 1:
         warmup = warmup * epochs
     warmup = int(warmup)
@@ -252,7 +269,12 @@ def train(
         for batch_idx in range(0, n, batch_size):
             rows = min(batch_size, n - batch_idx)
             if rows < world:
+                trainer._step_local(X_dev.ptr + batch_idx * D * 4,
+                                    None if C_dev is None else C_dev.ptr + batch_idx * Cd * 4, rows)
                 continue
+            if rows % world and epoch == 0:
+                warnings.warn(f"batch of {rows} rows does not split evenly over {world} ranks: ranks stay "
+                              "identical but their fp64 reduction order differs from one device's", RuntimeWarning)
             lo, hi = shard_rows(rows, rank, world)
             trainer._step_rows(X_dev.ptr + (batch_idx + lo) * D * 4,
                                None if C_dev is None else C_dev.ptr + (batch_idx + lo) * Cd * 4, hi - lo, rows)
