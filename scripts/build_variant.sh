@@ -7,7 +7,7 @@ set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 mkdir -p tune
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-result -I/opt/rocm/include -Iinclude"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-result -I/opt/rocm/include -Iinclude -fno-slp-vectorize"
 /opt/rocm/bin/hipcc $FLAGS "$@" -c -o tune/k16_$NAME.o zenflow_amd/csrc/zf_flow_x3_k16.hip
 OBJS=$(ls build/obj/*.o | grep -v zf_flow_x3_k16.o)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tune/lib$NAME.so $OBJS tune/k16_$NAME.o -ldl

@@ -271,19 +271,42 @@ def test_golden_edges(name):
 
 X3_SHAPES = ["cfg1", "cfg2", "cfg4", "cfg4c1", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
 X3_ACTS = [a for a in ACTS if a not in ("sigmoid", "softplus", "mixed_fp32")]
+BF16X3_ACTS = ["sigmoid", "softplus", "mixed_fp32"]  # bf16x3 by default (x3_scheme_for)
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ["small", "odd", "uniform"] + ACTS)
 def test_kernel_selection(name, monkeypatch):
     """relu, leaky_relu, tanh, gelu and elu run on f16x2 (its activation
-    switch); sigmoid and softplus, and every other activation under the
-    bf16x3 scheme, on the fp32 kernel (x3_eligible)."""
+    switch); a flow with a sigmoid or softplus coupling on bf16x3
+    (x3_scheme_for); every activation under ZF_X3_SCHEME=bf16x3 on bf16x3."""
     case = make_case(name, N=8, seed=30)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == ("f16x2" if name in X3_SHAPES + X3_ACTS else "fp32")
+    want = "f16x2" if name in X3_SHAPES + X3_ACTS else "bf16x3" if name in BF16X3_ACTS else "fp32"
+    assert bf.program.kernel_variant == want
     monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == ("bf16x3" if name in X3_SHAPES else "fp32")
+    assert bf.program.kernel_variant == ("bf16x3" if name in X3_SHAPES + ACTS else "fp32")
+
+
+@pytest.mark.parametrize("name", ACTS)
+def test_bf16x3_activation_parity(name, monkeypatch):
+    """NeuralSplineCoupling.act (bijectors.py:319, 345) on the bf16x3 split
+    kernel: sigmoid / softplus by default, the others under ZF_X3_SCHEME."""
+    if name not in BF16X3_ACTS:
+        monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
+    case = make_case(name, N=3000, seed=37)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "bf16x3"
+    check_lp(gpu_log_prob(case), case, f"bf16x3/{name}")
+    rng = np.random.default_rng(38)
+    z = (0.5 + 0.1 * rng.standard_normal(case["x"].shape)).astype(F32)
+    sub = {k: v["bijector"] for k, v in case["variables"].items()}
+    x = build_flow(case["cfg"]).bijector.apply(sub, z, case["c"], method="inverse")
+    ref = O.flow_inverse(case["model"], case["variables"], z, case["c"])
+    fin = np.isfinite(ref)
+    assert np.mean(fin != np.isfinite(x)) <= 1e-3
+    both = fin & np.isfinite(x)
+    assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
 
 
 @pytest.mark.parametrize("name", X3_SHAPES + ACTS)
@@ -335,11 +358,13 @@ def test_split_scaling_extremes(scheme, name, regime, monkeypatch):
     check_lp(gpu_log_prob(case), case, f"{scheme}/{name}/{regime}")
 
 
-@pytest.mark.parametrize("name", X3_ACTS)
+@pytest.mark.parametrize("name", X3_ACTS + BF16X3_ACTS)
 @pytest.mark.parametrize("regime", ["huge_activations", "tiny_activations", "tiny_weights", "huge_weights"])
 def test_split_scaling_extremes_other_acts(name, regime):
     """The same magnitude regimes on the f16x2 activation switch (every
-    activation it takes is bounded by |v|, x3_act_scale)."""
+    activation it takes is bounded by |v|, x3_act_scale), and on bf16x3 for
+    sigmoid / softplus (tiny pre-activations amplified by large weights: the
+    regime f16x2 resolves worse than fp32)."""
     case = make_case(name, N=1500, seed=36)
     params = case["variables"]["params"]["bijector"]
     for key, p in params.items():
@@ -357,7 +382,7 @@ def test_split_scaling_extremes_other_acts(name, regime):
             last = f"Dense_{len(case['cfg']['layers'])}"
             p[last]["kernel"] = (p[last]["kernel"] * 1e-5).astype(F32)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == "f16x2"
+    assert bf.program.kernel_variant == ("bf16x3" if name in BF16X3_ACTS else "f16x2")
     check_lp(gpu_log_prob(case), case, f"{name}/{regime}")
 
 

@@ -187,3 +187,36 @@ def test_rqs_golden():
         xi = u.rational_quadratic_spline_inverse(d["y"], d["dx"], d["dy"], d["slope"])
         fin = np.isfinite(d["x_inv"])
         assert_allclose(xi[fin], d["x_inv"][fin], rtol=1e-5, atol=1e-5, err_msg=f.name)
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 8, 40])
+@pytest.mark.parametrize("monotone", [True, False])
+def test_rqs_k32_two_lane_matches_one_lane(N, monotone, monkeypatch):
+    """K = 32 runs two lanes per item (rqs_kernel_pair: lane 1 continues lane
+    0's in-order knot sums): the same bits as the one-lane kernel
+    (ZF_K1_ONE_LANE=1), forward, log_det (lane-shuffle rows, N <= 32, and the
+    LDS rows, N = 40) and inverse, on normalised and on raw (non-monotone
+    knots: the generic-search fallback) parameters."""
+    u = _zu()
+    K = 32
+    rng = np.random.default_rng(900 + N)
+    M = 2051
+    if monotone:
+        dx, dy, sl = random_params(rng, M, N, K, scale=1.5)
+    else:
+        dx = (0.06 * rng.standard_normal((M, N, K)) + 0.03).astype(F32)
+        dy = (0.06 * rng.standard_normal((M, N, K)) + 0.03).astype(F32)
+        sl = np.abs(rng.standard_normal((M, N, K - 1))).astype(F32) + 0.1
+    x = rng.uniform(-0.1, 1.1, size=(M, N)).astype(F32)
+    y2, ld2 = u.rational_quadratic_spline_forward(x, dx, dy, sl)
+    xi2 = u.rational_quadratic_spline_inverse(x, dx, dy, sl)
+    monkeypatch.setenv("ZF_K1_ONE_LANE", "1")
+    y1, ld1 = u.rational_quadratic_spline_forward(x, dx, dy, sl)
+    xi1 = u.rational_quadratic_spline_inverse(x, dx, dy, sl)
+    assert np.array_equal(y1, y2, equal_nan=True)
+    assert np.array_equal(ld1, ld2, equal_nan=True)
+    assert np.array_equal(xi1, xi2, equal_nan=True)
+    if not monotone:  # and the oracle agrees where it is finite
+        yr, _ = O.rqs_forward(x, dx, dy, sl)
+        fin = np.isfinite(yr) & np.isfinite(y2)
+        assert_allclose(y2[fin], yr[fin], rtol=2e-6, atol=2e-6)

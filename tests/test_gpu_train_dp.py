@@ -30,7 +30,7 @@ def test_two_ranks_match_one_device_bitwise(tmp_path, name, N, seed):
     from zenflow_amd import _lib as L
     from zenflow_amd.launch import spawn
 
-    env = dict(os.environ, ZF_TEST_CASE=f"{name}:{N}:{seed}", ZF_TEST_STEPS="3")
+    env = dict(os.environ, ZF_TEST_CASE=f"{name}:{N}:{seed}", ZF_TEST_STEPS="3", ZF_DEVICE="0")
     assert spawn(2, [WORKER, "train_dp", str(tmp_path)], env=env, timeout=240) == 0
     ranks = [np.load(tmp_path / f"rank{k}.npz") for k in range(2)]
 
@@ -57,7 +57,7 @@ def test_train_function_two_ranks_match_one_device(tmp_path):
     from zenflow_amd.io import flatten_variables
     from zenflow_amd.launch import spawn
 
-    env = dict(os.environ, ZF_TEST_EPOCHS="20")
+    env = dict(os.environ, ZF_TEST_EPOCHS="20", ZF_DEVICE="0")
     assert spawn(2, [WORKER, "train_fn", str(tmp_path)], env=env, timeout=300) == 0
     X = two_moons_data()
     best, best_epoch, lt, ls = zf.train(two_moons_flow(), X[:2400], X[2400:], epochs=20, batch_size=512,
@@ -71,12 +71,12 @@ def test_train_function_two_ranks_match_one_device(tmp_path):
             assert np.array_equal(r["v:" + name], v), f"rank {k}: {name}"
 
 
-def _train_fn_ranks(tmp_path, ntrain, epochs=8):
+def _train_fn_ranks(tmp_path, ntrain, epochs=20):
     from tests.dist_worker import two_moons_data, two_moons_flow
     from zenflow_amd.launch import spawn
     import zenflow_amd as zf
 
-    env = dict(os.environ, ZF_TEST_EPOCHS=str(epochs), ZF_TEST_NTRAIN=str(ntrain))
+    env = dict(os.environ, ZF_TEST_EPOCHS=str(epochs), ZF_TEST_NTRAIN=str(ntrain), ZF_DEVICE="0")
     assert spawn(2, [WORKER, "train_fn", str(tmp_path)], env=env, timeout=300) == 0
     X = two_moons_data()
     one = zf.train(two_moons_flow(), X[:ntrain], X[2400:], epochs=epochs, batch_size=512, progress=False)
@@ -127,6 +127,7 @@ def test_rccl_two_ranks_match_one_device_bitwise(tmp_path):
     if not L.load_library().zf_rccl_available():
         pytest.skip("librccl not present on this box")
     env = dict(os.environ, ZF_TEST_CASE="cfg2:4096:91", ZF_TEST_STEPS="3")
+    env.pop("ZF_DEVICE", None)  # one GPU per rank (LOCAL_RANK)
     assert spawn(2, [WORKER, "train_rccl", str(tmp_path)], env=env, timeout=240) == 0
     ranks = [np.load(tmp_path / f"rank{k}.npz") for k in range(2)]
     case, flow, tr = _setup("cfg2", 4096, 91)

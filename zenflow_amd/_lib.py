@@ -221,7 +221,9 @@ def ensure_device() -> None:
             "zenflow_amd: no HIP device is visible; the product path runs only on "
             "MI355X (gfx950) and has no CPU fallback."
         )
-    dev = int(os.environ.get("LOCAL_RANK", os.environ.get("ZF_DEVICE", "0")))
+    # ZF_DEVICE (explicit) wins over LOCAL_RANK (one rank per GPU); ranks
+    # that share one GPU on purpose (HostAllgather tests) set ZF_DEVICE
+    dev = int(os.environ.get("ZF_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     n = device_count()
     if not 0 <= dev < n:
         # one process per GPU: an oversubscribed or mis-masked launch would put

@@ -38,13 +38,22 @@ FLAGS = [
     f"-I{INCLUDE}",
 ]
 
+# Split-MFMA kernel translation units: no SLP packing of scalar f32 ops into
+# v_pk_* (packed f32 VALU beside MFMAs costs more issue than two scalar ops;
+# cfg2 -1% kernel time)
+X3_FLAGS = ["-fno-slp-vectorize"]
+
+
+def _src_flags(src: str):
+    return X3_FLAGS if src.startswith("zf_flow_x3_k") else []
+
 
 def _fingerprint() -> str:
     h = hashlib.sha256()
     for f in SOURCES + HEADERS:
         h.update((CSRC / f).read_bytes())
     h.update((INCLUDE / "zenflow_amd.h").read_bytes())
-    h.update(" ".join(FLAGS).encode())
+    h.update(" ".join(FLAGS + X3_FLAGS).encode())
     return h.hexdigest()
 
 
@@ -62,7 +71,7 @@ def build(force: bool = False, verbose: bool = True, out: Path = LIB, extra=()) 
 
     def _compile(src: str) -> Path:
         obj = objdir / (Path(src).stem + ".o")
-        cmd = [HIPCC, *compile_flags, "-c", "-o", str(obj), str(CSRC / src)]
+        cmd = [HIPCC, *compile_flags, *_src_flags(src), "-c", "-o", str(obj), str(CSRC / src)]
         if verbose:
             print("[zenflow_amd.build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -602,7 +602,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
     }
   }
   std::vector<uint16_t> x3s;
-  const int NT = zf::x3_scheme();
+  const int NT = zf::x3_scheme_for(desc);
   if (x3) {
     // each NSC's small parameters [bn, end of the permuted last bias) as whole
     // 1 KiB DMA pieces (the blob allocation carries 1 KiB of slack past its end)

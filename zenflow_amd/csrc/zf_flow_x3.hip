@@ -44,16 +44,13 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind != ZF_OP_NSC) continue;
-    // Activations other than swish: f16x2 only (the bf16x3 reference scheme
-    // keeps swish), and only those with act(0) = 0 and |act(v)| <= |v|
-    // (relu, leaky_relu, tanh, gelu, elu): the per-sample power-of-two scale
-    // then keeps every value's relative precision.  sigmoid and softplus
+    // Any activation: relu, leaky_relu, tanh, gelu and elu (act(0) = 0,
+    // |act(v)| <= |v|: the f16x2 per-sample power-of-two scale keeps every
+    // value's relative precision) run on either scheme; sigmoid and softplus
     // carry their information as small deviations from 1/2 and log 2, which
     // 22-bit split operands resolve worse than fp32 (measured: 1e-3 relative
-    // on tiny pre-activations amplified by large weights); they stay on the
-    // fp32 kernel.
-    const int a = op.act;
-    if (a != ZF_ACT_SWISH && (x3_scheme() != 2 || a == ZF_ACT_SIGMOID || a == ZF_ACT_SOFTPLUS)) return false;
+    // on tiny pre-activations amplified by large weights), so a flow with
+    // one of them runs the scaling-free bf16x3 scheme (x3_scheme_for).
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }
@@ -68,6 +65,17 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
 int x3_scheme() {
   const char* env = std::getenv("ZF_X3_SCHEME");
   if (env && std::strcmp(env, "bf16x3") == 0) return 3;
+  return 2;
+}
+
+// The scheme of one flow: bf16x3 when asked for, or when a coupling's
+// activation is sigmoid or softplus (x3_eligible); f16x2 otherwise.
+int x3_scheme_for(const zf_flow_desc& desc) {
+  if (x3_scheme() == 3) return 3;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind == ZF_OP_NSC && (op.act == ZF_ACT_SIGMOID || op.act == ZF_ACT_SOFTPLUS)) return 3;
+  }
   return 2;
 }
 

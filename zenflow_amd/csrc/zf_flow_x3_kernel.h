@@ -225,13 +225,32 @@ __device__ __forceinline__ void act_tile_fixed(floatx16& t, float c) {
   for (int r = 0; r < 16; ++r) t[r] = act_other(CODE, t[r]) * c;
 }
 
+template <int CODE>
+__device__ __forceinline__ void act_tile_plain(floatx16& t) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] = act_other(CODE, t[r]);
+}
+
 template <int NT, bool OACT>
 __device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
   if constexpr (!OACT) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+  } else if constexpr (NT == 3) {
+    // bf16x3: no scales; every activation, sigmoid and softplus included
+    switch (act) {
+      case ZF_ACT_RELU: act_tile_plain<ZF_ACT_RELU>(t); break;
+      case ZF_ACT_TANH: act_tile_plain<ZF_ACT_TANH>(t); break;
+      case ZF_ACT_SIGMOID: act_tile_plain<ZF_ACT_SIGMOID>(t); break;
+      case ZF_ACT_GELU: act_tile_plain<ZF_ACT_GELU>(t); break;
+      case ZF_ACT_SOFTPLUS: act_tile_plain<ZF_ACT_SOFTPLUS>(t); break;
+      case ZF_ACT_ELU: act_tile_plain<ZF_ACT_ELU>(t); break;
+      case ZF_ACT_LEAKY_RELU: act_tile_plain<ZF_ACT_LEAKY_RELU>(t); break;
+      default:
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t[r] = swish(t[r]);
+    }
   } else {
-    static_assert(NT == 2, "other activations run on the f16x2 scheme");
     switch (act) {
       case ZF_ACT_RELU: act_tile_fixed<ZF_ACT_RELU>(t, c); break;
       case ZF_ACT_TANH: act_tile_fixed<ZF_ACT_TANH>(t, c); break;
@@ -762,11 +781,6 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
   p.tbar += X3T_NOW() - tb0;
 #endif
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
-  floatx16 bt[NOUT];
-  if constexpr (HASB) {
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-  }
   const char* lb = p.cur + lane * 16;
   halfx8 fr[2][NT];
   load_frag<NT>(lb, fr[0]);
@@ -788,8 +802,11 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
                            s1h, csh, isc);
   static_assert(kSlots >= 2, "at least one triple per k-step");
   if constexpr (HASB) {
+    // the layer end, acc * us + bias, one fma per value; the bias tiles are
+    // read here, when the layer's input tiles are dead (no registers held
+    // across the group's MFMAs)
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bias_acc(bias + o * 32, hh));
   }
   char* const t = p.cur;
   p.cur = p.nxt;
@@ -843,7 +860,7 @@ __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p,
 // relative to op.bn) and the conditions from the per-wave state (columns D..)
 // — no global load on the per-coupling path, so no vmcnt wait there drains
 // the weight-group DMA in flight.
-template <int T>
+template <int T, bool OACT>
 __device__ __forceinline__ void x3_layer0(const X3Sc& c, const float* par, const float* xs, int rot, int D,
                                           int s, int hh, int lane, floatx16 (&hb)[T], int swish_tiles) {
   const int dt = c.dt, dc = c.dc, DC = c.DC, KS0 = c.KS0;
@@ -865,9 +882,14 @@ __device__ __forceinline__ void x3_layer0(const X3Sc& c, const float* par, const
   }
 #pragma unroll
   for (int o = 0; o < T; ++o)
-    if (o < swish_tiles)
+    if (o < swish_tiles) {  // bf16x3 only (f16x2 passes 0)
+      if constexpr (OACT) {
+        x3_act_tile<3, true>(hb[o], 1.f, c.act);
+      } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
+        for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
+      }
+    }
 }
 
 // Spline arithmetic of the split-MFMA kernel: the spline parameters already differ from the reference's in the last ulp
@@ -1046,12 +1068,20 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       constexpr bool kPipe = T == 4 && !PAIRS;
       // f16x2: every layer leaves raw pre-activations; the next streamed
       // layer scales and swishes them (act_swish) as it goes.
-      x3_layer0<T>(opc, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (nh > 1 || kLastSW) ? 1 : T);
+      // bf16x3 OACT: every tile's activation at the layer end (no switch inside
+      // the group steps)
+      x3_layer0<T, OACT>(opc, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (!OACT && (nh > 1 || kLastSW)) ? 1 : T);
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
       // biases seed the accumulators.  f16x2: they seed them divided by the
       // unscale (exact: powers of two) and the accumulators are multiplied
       // by it afterwards (kSeedScaled).
-      constexpr bool kSeedScaled = NT == 2;
+#ifndef ZF_X3_SEEDSCALED
+#define ZF_X3_SEEDSCALED 0
+#endif
+      // f16x2 at hidden 128 (the slot schedule): zero-seeded accumulators and
+      // one fma per value at the layer end (acc * us + bias) instead of a
+      // bias * ius seed and an acc * us unscale (two multiplies per value)
+      constexpr bool kSeedScaled = NT == 2 && (ZF_X3_SEEDSCALED || !kPipe || OACT);
       // Three waves share a SIMD at hidden 128: the one streaming weight
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
       // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
@@ -1088,12 +1118,17 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
           for (int o = 0; o < T; ++o) acc[o] *= us;
         }
-        const int nsw = NT == 2 ? 0 : (l + 1 < nh || kLastSW) ? 1 : T;
+        const int nsw = NT == 2 ? 0 : (!OACT && (l + 1 < nh || kLastSW)) ? 1 : T;
 #pragma unroll
         for (int o = 0; o < T; ++o) {
           if (o < nsw) {
+            if constexpr (OACT) {
+              hb[o] = acc[o];
+              x3_act_tile<3, true>(hb[o], 1.f, act);
+            } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
+              for (int r = 0; r < 16; ++r) hb[o][r] = swish(acc[o][r]);
+            }
           } else {
             hb[o] = acc[o];
           }

@@ -189,6 +189,116 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
   }
 }
 
+// Two lanes per (row, dim) item (K = 32): lane p of a pair loads knots
+// 16p..16p+15 (the pair reads one contiguous 128-B row per array, half the
+// registers of the one-lane form, so twice the waves stream), and sweeps
+// them from the partner's prefix: lane 0 sums its 16 widths / heights in
+// order and lane 1 continues the same sequential sums from there (the knots
+// carry the one-lane form's bits).  The bin comes from lane 1 when any of its
+// knots (16..32) is <= v, else from lane 0; non-monotone knots fall back to
+// the generic search (rqs_bin).  Both lanes evaluate, lane 0 stores.
+struct GlobalParams {
+  const float* dx;
+  const float* dy;
+  const float* sl;
+  __device__ float w(int j) const { return dx[j]; }
+  __device__ float h(int j) const { return dy[j]; }
+  __device__ float d(int j) const { return sl[j]; }
+};
+
+template <bool FWD, int K>
+__global__ __launch_bounds__(kK1Threads) void rqs_kernel_pair(
+    const float* __restrict__ xin, const float* __restrict__ dx, const float* __restrict__ dy,
+    const float* __restrict__ slope, float* __restrict__ out, float* __restrict__ log_det,
+    int64_t M, int N, int R) {
+  constexpr int KH = K / 2, Q = KH / 4;
+  __shared__ float s_ld[kK1Threads / 2];
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int64_t left = M - r0;
+  const int rows = (int)(left < R ? left : R);
+  const int items = rows * N;
+  const int tid = threadIdx.x;
+  const int it = tid >> 1, p = tid & 1;
+  const int64_t item = r0 * N + min(it, items - 1);  // clamped: loads stay unconditional
+  const float4* rw = reinterpret_cast<const float4*>(dx + item * K + KH * p);
+  const float4* rh = reinterpret_cast<const float4*>(dy + item * K + KH * p);
+  float w[KH], h[KH];
+#pragma unroll
+  for (int c = 0; c < Q; ++c) {
+    const float4 a = rw[c];
+    const float4 b = rh[c];
+    w[4 * c] = a.x; w[4 * c + 1] = a.y; w[4 * c + 2] = a.z; w[4 * c + 3] = a.w;
+    h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
+  }
+  const float v = xin[item];
+  // lane 0's knot 16 = its in-order sums; lane 1 starts from them
+  float ex = 0.f, ey = 0.f;
+#pragma unroll
+  for (int j = 0; j < KH; ++j) { ex = ex + w[j]; ey = ey + h[j]; }
+  const float px = __shfl_xor(ex, 1), py = __shfl_xor(ey, 1);
+  float xk = p ? px : 0.f, yk = p ? py : 0.f;
+  float sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
+  int cnt = 0, sel = 0;
+#pragma unroll
+  for (int j = 0; j < KH; ++j) {
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = KH * p + j; sxk = xk; syk = yk; sw = w[j]; sh = h[j]; }
+    xk = xk + w[j];
+    yk = yk + h[j];
+  }
+  if (p) {  // the last knot (K)
+    const float kk = FWD ? xk : yk;
+    if (kk <= v) { ++cnt; sel = K; sxk = xk; syk = yk; sw = qnan(); sh = qnan(); }
+  }
+  // lane 1's data where it has a hit, else lane 0's
+  const int ocnt = __shfl_xor(cnt, 1), osel = __shfl_xor(sel, 1);
+  const float oxk = __shfl_xor(sxk, 1), oyk = __shfl_xor(syk, 1), ow = __shfl_xor(sw, 1), oh = __shfl_xor(sh, 1);
+  const int c1 = p ? cnt : ocnt;
+  const bool own = p ? (c1 > 0) : (c1 == 0);
+  RqsBin b;
+  const int bsel = own ? sel : osel;
+  b.xk = own ? sxk : oxk;
+  b.yk = own ? syk : oyk;
+  b.w = own ? sw : ow;
+  b.h = own ? sh : oh;
+  const int tot = cnt + ocnt;
+  int idx = tot - 1;
+  idx = idx < 0 ? 0 : (idx > K ? K : idx);
+  const float* slp = slope + item * (K - 1);
+  if (idx != bsel) {  // non-monotone knots (never from normalize_spline_params)
+    b = rqs_bin<FWD>(v, K, GlobalParams{dx + item * K, dy + item * K, slp});
+  } else {
+    b.dk = (bsel == 0 || bsel == K) ? 1.0f : slp[bsel - 1];
+    b.dkp1 = (bsel + 1 < K) ? slp[bsel] : (bsel + 1 == K ? 1.0f : qnan());
+    b.sk = b.h / b.w;
+    b.oob = (v < 0.f) || (v >= 1.f);
+  }
+  if (FWD) {
+    float y, l;
+    rqs_forward_eval(v, b, y, l);
+    if (p == 0 && it < items && out) out[item] = y;
+    if (log_det) {
+      if (N <= 32 && (N & (N - 1)) == 0) {
+        // a row's N items sit on 2N consecutive lanes: sum in dim order
+        const int lane = tid & 63, base = lane & ~(2 * N - 1);
+        float acc = 0.f;
+        for (int n = 0; n < N; ++n) acc = acc + __shfl(l, base + 2 * n);
+        if (lane == base && it < items) log_det[r0 + it / N] = acc;
+      } else {
+        if (p == 0 && it < items) s_ld[it] = l;
+        __syncthreads();
+        if (tid < rows) {
+          float acc = 0.f;  // log_det.sum(axis=1), dim order
+          for (int n = 0; n < N; ++n) acc = acc + s_ld[tid * N + n];
+          log_det[r0 + tid] = acc;
+        }
+      }
+    }
+  } else if (p == 0 && it < items) {
+    out[item] = rqs_inverse_eval(v, b);
+  }
+}
+
 // Row-wise utils kernels (thresholded softmax, normalize_spline_params):
 // one thread per row, but the block's rows (contiguous in HBM) are staged
 // through LDS with coalesced loads and stores (odd row stride) — a thread
@@ -366,6 +476,15 @@ int launch_rqs(const float* x, const float* dx, const float* dy, const float* sl
   if (!FWD && !out) return einval("NULL output");
   hipStream_t st = (hipStream_t)stream;
   const bool aligned = ((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
+  if (aligned && K == 32 && N <= kK1Threads / 2 && std::getenv("ZF_K1_ONE_LANE") == nullptr) {
+    const int R = (kK1Threads / 2) / N;
+    const int64_t grid = (M + R - 1) / R;
+    if (grid > 0x7fffffffLL) return einval("M too large");
+    hipLaunchKernelGGL((rqs_kernel_pair<FWD, 32>), dim3((unsigned)grid), dim3(kK1Threads), 0, st, x, dx, dy, slope,
+                       out, log_det, M, N, R);
+    ZF_CHECK_LAUNCH("rqs_kernel_pair");
+    return ZF_OK;
+  }
   if (aligned && (K == 4 || K == 8 || K == 16 || K == 32) && N <= kK1Threads) {
     const int R = kK1Threads / N;
     const int64_t grid = (M + R - 1) / R;
