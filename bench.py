@@ -58,6 +58,8 @@ WORKLOADS = {
     # cfg2 with NeuralSplineCoupling(act=...) other than swish (bijectors.py:319)
     "cfg2relu": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "relu"),
     "cfg2gelu": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "gelu"),
+    "cfg2sigmoid": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "sigmoid"),
+    "cfg2softplus": (4, 0, 16, (128, 128), 4, "normal", "log_prob", "softplus"),
 }
 
 

@@ -44,13 +44,17 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind != ZF_OP_NSC) continue;
-    // Any activation: relu, leaky_relu, tanh, gelu and elu (act(0) = 0,
-    // |act(v)| <= |v|: the f16x2 per-sample power-of-two scale keeps every
-    // value's relative precision) run on either scheme; sigmoid and softplus
-    // carry their information as small deviations from 1/2 and log 2, which
-    // 22-bit split operands resolve worse than fp32 (measured: 1e-3 relative
-    // on tiny pre-activations amplified by large weights), so a flow with
-    // one of them runs the scaling-free bf16x3 scheme (x3_scheme_for).
+    // relu, leaky_relu, tanh, gelu and elu (act(0) = 0, |act(v)| <= |v|: the
+    // f16x2 per-sample power-of-two scale keeps every value's relative
+    // precision) run on either scheme.  sigmoid carries its information as
+    // small deviations from 1/2, which f16x2's 22-bit split operands resolve
+    // worse than fp32 (1e-3 relative on tiny pre-activations amplified by
+    // large weights), so a flow with a sigmoid coupling runs the scaling-free
+    // bf16x3 scheme (x3_scheme_for).  softplus stays on the fp32 kernel: in
+    // the same regime (deviations from log 2 under 1e4-scale weights, a
+    // cancellation of 1e3-size products) bf16x3's mean error was 5x the
+    // fp32 oracle's, the fp32 kernel's equal to it (scripts/diag_acts.py).
+    if (op.act == ZF_ACT_SOFTPLUS) return false;
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }
@@ -69,12 +73,12 @@ int x3_scheme() {
 }
 
 // The scheme of one flow: bf16x3 when asked for, or when a coupling's
-// activation is sigmoid or softplus (x3_eligible); f16x2 otherwise.
+// activation is sigmoid (x3_eligible); f16x2 otherwise.
 int x3_scheme_for(const zf_flow_desc& desc) {
   if (x3_scheme() == 3) return 3;
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
-    if (op.kind == ZF_OP_NSC && (op.act == ZF_ACT_SIGMOID || op.act == ZF_ACT_SOFTPLUS)) return 3;
+    if (op.kind == ZF_OP_NSC && op.act == ZF_ACT_SIGMOID) return 3;
   }
   return 2;
 }

@@ -231,6 +231,20 @@ __device__ __forceinline__ void act_tile_plain(floatx16& t) {
   for (int r = 0; r < 16; ++r) t[r] = act_other(CODE, t[r]);
 }
 
+// bf16x3 sigmoid: 1 / (1 + 2^(-v log2 e)) from the hardware exp2 and a
+// residual-corrected reciprocal (8 VALU instead of expf + IEEE division);
+// 1 + e = inf (v < -88) gives 0, as 1 / (1 + expf(-v)) does.
+template <>
+__device__ __forceinline__ void act_tile_plain<ZF_ACT_SIGMOID>(floatx16& t) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float d = 1.0f + __builtin_amdgcn_exp2f(-t[r] * kSwishPrescale);
+    const float q = __builtin_amdgcn_rcpf(d);
+    const float c = __builtin_fmaf(q, __builtin_fmaf(-d, q, 1.0f), q);
+    t[r] = d == __builtin_huge_valf() ? 0.0f : c;  // NaN stays NaN
+  }
+}
+
 template <int NT, bool OACT>
 __device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
   if constexpr (!OACT) {
