@@ -203,3 +203,27 @@ def test_module_variable_updates():
     assert out == 4 and upd["batch_stats"]["count"]["n"] == 4 and v["batch_stats"]["count"]["n"] == 2
     with pytest.raises(RuntimeError):
         m.apply(v)
+
+
+def test_activation_callables_recognised_by_value():
+    """NeuralSplineCoupling.act is any callable (bijectors.py:319): a lambda
+    that computes a supported activation maps to its kernel code; anything
+    else is rejected (no silent fallback)."""
+    from zenflow_amd import _lib as L
+    from zenflow_amd.activations import act_code
+
+    assert act_code(lambda x: x / (1 + np.exp(-x))) == L.ZF_ACT_SWISH
+    assert act_code(lambda x: x * (1 / (1 + np.exp(-x)))) == L.ZF_ACT_SWISH
+    assert act_code(lambda x: np.maximum(x, 0.0)) == L.ZF_ACT_RELU
+    assert act_code(lambda v: np.where(v >= 0, v, 0.01 * v)) == L.ZF_ACT_LEAKY_RELU
+    assert act_code(lambda v: np.log1p(np.exp(-np.abs(v))) + np.maximum(v, 0)) == L.ZF_ACT_SOFTPLUS
+    assert act_code(lambda v: np.tanh(v)) == L.ZF_ACT_TANH
+    with pytest.raises(NotImplementedError):
+        act_code(lambda v: np.sin(v))
+    with pytest.raises(NotImplementedError):
+        act_code(lambda v: v * 1.5)  # close to none of them
+    with pytest.raises(NotImplementedError):
+        act_code("mish")
+    # a coupling built with such a callable packs the kernel's activation
+    nsc = bi.NeuralSplineCoupling(knots=8, layers=(16,), act=lambda x: np.maximum(x, 0.0))
+    assert act_code(nsc.act) == L.ZF_ACT_RELU
