@@ -204,7 +204,8 @@ def spline_kernel_roofline(M, N, K, steps):
             kname = "normalize_vec_kernel"
         else:
             nbytes = M * (N * (4 * 3 * K + 4) + (4 if tag == "forward" else 0))
-            kname = "rqs_kernel_direct" if K in (4, 8, 16, 32) else "rqs_kernel"
+            kname = ("rqs_kernel_pair" if K == 32 and N <= 128 and not os.environ.get("ZF_K1_ONE_LANE")
+                     else "rqs_kernel_direct" if K in (4, 8, 16, 32) else "rqs_kernel")
         gbs = nbytes / t / 1e9
         out[tag] = {"kernel": kname, "shape": [M, N, K], "us": t * 1e6, "alg_bytes": nbytes,
                     "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS}
@@ -600,6 +601,8 @@ def main():
                                         "kernel, device->host copy and Python dispatch; cached device program"}
     if not args.no_spline_kernel and rank == 0:
         result["spline_kernel"] = spline_kernel_roofline(N, 2, K, args.steps)
+        if K != 32:  # K1 at 32 knots too (the two-lanes-per-item kernel)
+            result["spline_kernel_k32"] = spline_kernel_roofline(N, 2, 32, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         spec = oracle_spec(name)
         if mode in ("log_prob", "apply"):
