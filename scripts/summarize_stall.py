@@ -47,6 +47,14 @@ def main(tag="r02", src=ROOT / "gpurun_out"):
     }
     out["simd_idle"] = 1 - out["mfma_busy"] - out["valu_issue"] + out["valu_mfma_coexec"]
     (ROOT / "profiles" / f"{tag}_x3_stall_counters.json").write_text(json.dumps(out, indent=1) + "\n")
+    # the bench line's roofline.valu_mfma_coexec (profiles/pmc_traffic.json)
+    tf = ROOT / "profiles" / "pmc_traffic.json"
+    if tf.exists():
+        t = json.loads(tf.read_text())
+        if "flow_kernel_x3" in t:
+            t["flow_kernel_x3"]["valu_mfma_coexec"] = out["valu_mfma_coexec"]
+            t["flow_kernel_x3"]["stall_source"] = f"profiles/{tag}_x3_stall_counters.json"
+            tf.write_text(json.dumps(t, indent=1) + "\n")
     print(json.dumps({k: v for k, v in out.items() if k != "counters_median"}, indent=1))
 
 
