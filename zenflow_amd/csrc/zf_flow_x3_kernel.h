@@ -1096,6 +1096,14 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // one fma per value at the layer end (acc * us + bias) instead of a
       // bias * ius seed and an acc * us unscale (two multiplies per value)
       constexpr bool kSeedScaled = NT == 2 && (ZF_X3_SEEDSCALED || !kPipe || OACT);
+      // the hidden layers of a dim-pair flow (d8, d16: PAIRS, 2 waves per
+      // SIMD) take the f16x2 slot schedule too: only the last layer, which
+      // re-reads its input once per pair, keeps the plain group steps
+#ifndef ZF_X3_PAIRS_PIPE
+#define ZF_X3_PAIRS_PIPE 1
+#endif
+      constexpr bool kPipeH = kPipe || (ZF_X3_PAIRS_PIPE && T == 4 && NT == 2 && !OACT);
+      constexpr bool kSeedScaledH = NT == 2 && (ZF_X3_SEEDSCALED || !kPipeH || OACT);
       // Three waves share a SIMD at hidden 128: the one streaming weight
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
       // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
@@ -1118,17 +1126,17 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
         for (int o = 0; o < T; ++o)
           acc[o] = NT == 3 ? bias_acc(bl_l + o * 32, hh)
-                           : (kSeedScaled ? bias_acc(bl_l + o * 32, hh) * ius : floatx16{0});
-        const float* bh = (NT == 2 && !kSeedScaled) ? bl_l : nullptr;
-        if constexpr (kPipe) {
+                           : (kSeedScaledH ? bias_acc(bl_l + o * 32, hh) * ius : floatx16{0});
+        const float* bh = (NT == 2 && !kSeedScaledH) ? bl_l : nullptr;
+        if constexpr (kPipeH) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
-          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaled, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
+          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaledH, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
                                                                  act);
         } else {
           x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, act);
         }
-        if constexpr (kSeedScaled) {
+        if constexpr (kSeedScaledH) {
 #pragma unroll
           for (int o = 0; o < T; ++o) acc[o] *= us;
         }
