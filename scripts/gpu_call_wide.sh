@@ -1,0 +1,8 @@
+#!/bin/bash
+# One gpurun call: A/B of the slot schedule at hidden 256 (cfg5), then the
+# hidden-256 parity tests on that build (ZF_LIB).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+LIBS="w0 w1" ROUNDS=2 BENCH_ARGS="--config cfg5" STEPS=10 bash scripts/ab_libs.sh 2>&1 | tee gpurun_out/ab_wide.txt || exit 1
+ZF_LIB=tune/libw1.so timeout -k 10 600 python -u -m pytest -q -p no:cacheprovider --timeout 240 --timeout-method thread tests/test_gpu_flow.py tests/test_gpu_sampling.py -k "cfg5 or h256 or k32" > gpurun_out/pt_wide.log 2>&1; echo "pytest rc=$?"; tail -6 gpurun_out/pt_wide.log

@@ -1097,12 +1097,17 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // bias * ius seed and an acc * us unscale (two multiplies per value)
       constexpr bool kSeedScaled = NT == 2 && (ZF_X3_SEEDSCALED || !kPipe || OACT);
       // the hidden layers of a dim-pair flow (d8, d16: PAIRS, 2 waves per
-      // SIMD) take the f16x2 slot schedule too: only the last layer, which
-      // re-reads its input once per pair, keeps the plain group steps
+      // SIMD) and of hidden-256 flows (cfg5: T = 8, one wave per SIMD) take
+      // the f16x2 slot schedule too: only the last layer, which re-reads its
+      // input once per pair, keeps the plain group steps (d8 -2.1%, cfg5
+      // -3.4% kernel time)
+#ifndef ZF_X3_WIDE_PIPE
+#define ZF_X3_WIDE_PIPE 1
+#endif
 #ifndef ZF_X3_PAIRS_PIPE
 #define ZF_X3_PAIRS_PIPE 1
 #endif
-      constexpr bool kPipeH = kPipe || (ZF_X3_PAIRS_PIPE && T == 4 && NT == 2 && !OACT);
+      constexpr bool kPipeH = kPipe || (ZF_X3_PAIRS_PIPE && (T == 4 || ZF_X3_WIDE_PIPE) && NT == 2 && !OACT);
       constexpr bool kSeedScaledH = NT == 2 && (ZF_X3_SEEDSCALED || !kPipeH || OACT);
       // Three waves share a SIMD at hidden 128: the one streaming weight
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
