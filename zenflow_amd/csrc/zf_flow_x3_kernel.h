@@ -828,6 +828,45 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
   p.g += 1;
 }
 
+// Dim-pair last layer (PAIRS, f16x2): the layer input is split once, before
+// the pair loop (sp[tile][k-step] = hi / lo), so each pair's group steps are
+// MFMAs and fragment reads only (the plain steps re-split every tile per
+// pair).  A fragments one (k-step, tile) ahead.
+template <int T, int NOUT, int Q>
+__device__ __forceinline__ void x3_step_pre(const char* __restrict__ x3, X3Pipe& p, const halfx8 (&sp)[T][2][2],
+                                            floatx16 (&acc)[NOUT], int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<2, T>(x3, p, p.nxt, lane);
+  const char* lb = p.cur + lane * 16;
+  halfx8 c[2];
+  load_frag<2>(lb, c);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) {
+      const int t = s * NOUT + o;
+      halfx8 n[2];
+      if (t + 1 < 2 * NOUT) load_frag<2>(lb + (((t + 1) * 2) << 10), n);
+      acc[o] = mfma_split<2>(c, sp[Q][s], acc[o]);
+      if (t + 1 < 2 * NOUT) {
+        c[0] = n[0];
+        c[1] = n[1];
+      }
+    }
+  char* const tb = p.cur;
+  p.cur = p.nxt;
+  p.nxt = tb;
+  p.g += 1;
+}
+
+template <int T, int NOUT, int Q = 0>
+__device__ __forceinline__ void x3_layer_pre(const char* __restrict__ x3, X3Pipe& p, const halfx8 (&sp)[T][2][2],
+                                             floatx16 (&acc)[NOUT], int lane) {
+  x3_step_pre<T, NOUT, Q>(x3, p, sp, acc, lane);
+  if constexpr (Q + 1 < T) x3_layer_pre<T, NOUT, Q + 1>(x3, p, sp, acc, lane);
+}
+
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
 template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
@@ -1176,6 +1215,21 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         for (int o = 0; o < T; ++o)
           if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT>(hb[o], lisc, act);
       }
+#ifndef ZF_X3_PRESPLIT
+#define ZF_X3_PRESPLIT 1
+#endif
+      // PAIRS at hidden 128 (f16x2): the last layer's input split once for
+      // all pairs (d8 -1.0%; at hidden 256, one wave per SIMD, the per-pair
+      // re-split hides in the MFMA gaps and the pre-split cost 5.6%)
+      constexpr bool kPre = ZF_X3_PRESPLIT && PAIRS && T == 4 && NT == 2 && !OACT;
+      halfx8 sp[kPre ? T : 1][2][2];
+      if constexpr (kPre) {
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          split8h<0>(hb[q], sp[q][0][0], sp[q][0][1]);
+          split8h<1>(hb[q], sp[q][1][0], sp[q][1][1]);
+        }
+      }
       for (int pr = 0; pr < npair; ++pr) {
         // The bias seeds the accumulators when the hidden activations stay
         // live across pairs anyway; otherwise it joins in the last step, when
@@ -1188,7 +1242,9 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         for (int o = 0; o < TL; ++o)
           pa[o] = kSeed ? bias_acc(bl + o * 32, hh) : (kSeedScaled ? bias_acc(bl + o * 32, hh) * lius : floatx16{0});
         X3T(3);
-        if constexpr (kPipe) {
+        if constexpr (kPre) {
+          x3_layer_pre<T, TL>(x3, pipe, sp, pa, lane);
+        } else if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
           x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, act);
