@@ -15,23 +15,29 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+NCOUP = {"cfg2": 4, "cfg3": 4, "cfg3s": 4, "cfg4": 2, "cfg5": 8, "d8": 8, "cfg1": 2}  # NSC couplings per flow
 
 
-def main(tag="r02", src=ROOT / "gpurun_out"):
+def main(tag="r02", src=ROOT / "gpurun_out", prefix="pmc_st", label="cfg2"):
+    """prefix: the pmc_stall.sh PMC_PREFIX of the passes; label: the config
+    (cfg2 also refreshes the bench's pmc_traffic.json entry)."""
     agg = {}
-    for path in glob.glob(str(Path(src) / "pmc_st*" / "run_counter_collection.csv")):
+    kname = None
+    for path in glob.glob(str(Path(src) / f"{prefix}*" / "run_counter_collection.csv")):
         for r in csv.DictReader(open(path)):
             if "flow_kernel_x3" not in r["Kernel_Name"]:
                 continue
             if int(r.get("Grid_Size") or r["Grid_Size_X"]) < (1 << 20):
                 continue
             agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            kname = r["Kernel_Name"]
     med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
     cyc = med["GRBM_GUI_ACTIVE"] / 8
     simd = 1024 * cyc
     waves = med["SQ_WAVE_CYCLES"]
     out = {
-        "kernel": "flow_kernel_x3<2,16,4,false,false,false> (cfg2), grid 2^20 rows",
+        "kernel": (kname[kname.index("flow_kernel_x3"):kname.index(">") + 1] if kname else "flow_kernel_x3")
+        + f" ({label}), 2^20-row launches",
         "counters_median": med,
         "kernel_cycles": cyc,
         "mfma_busy": med["SQ_VALU_MFMA_BUSY_CYCLES"] / simd,
@@ -40,16 +46,18 @@ def main(tag="r02", src=ROOT / "gpurun_out"):
         "wave_active": med["SQ_ACTIVE_INST_ANY"] / waves,
         "wave_wait_inst_any": med["SQ_WAIT_INST_ANY"] / waves,
         "wave_wait_any": med["SQ_WAIT_ANY"] / waves,
-        "per_wave_coupling": {k: med[c] / 32768 / 4 for k, c in (
+        "couplings": NCOUP.get(label, 4),
+        "per_wave_coupling": {k: med[c] / med.get("SQ_WAVES", 32768) / NCOUP.get(label, 4) for k, c in (
             ("valu_insts", "SQ_INSTS_VALU"), ("mfma_insts", "SQ_INSTS_MFMA"), ("trans_f32_insts", "SQ_INSTS_VALU_TRANS_F32"),
             ("salu_insts", "SQ_INSTS_SALU"), ("lds_insts", "SQ_INSTS_LDS"), ("branches", "SQ_INSTS_BRANCH"))},
         "lds_bank_conflicts": med.get("SQ_LDS_BANK_CONFLICT"),
     }
     out["simd_idle"] = 1 - out["mfma_busy"] - out["valu_issue"] + out["valu_mfma_coexec"]
-    (ROOT / "profiles" / f"{tag}_x3_stall_counters.json").write_text(json.dumps(out, indent=1) + "\n")
+    name = f"{tag}_x3_stall_counters.json" if label == "cfg2" else f"{tag}_x3_stall_counters_{label}.json"
+    (ROOT / "profiles" / name).write_text(json.dumps(out, indent=1) + "\n")
     # the bench line's roofline.valu_mfma_coexec (profiles/pmc_traffic.json)
     tf = ROOT / "profiles" / "pmc_traffic.json"
-    if tf.exists():
+    if label == "cfg2" and tf.exists():
         t = json.loads(tf.read_text())
         if "flow_kernel_x3" in t:
             t["flow_kernel_x3"]["valu_mfma_coexec"] = out["valu_mfma_coexec"]

@@ -211,6 +211,39 @@ def device_count() -> int:
     return n.value if rc == 0 else 0
 
 
+def select_device(env, n: int) -> int:
+    """The device index this process binds (one rank per GPU).
+
+    * ``LOCAL_RANK`` (torchrun / our launcher) picks device LOCAL_RANK; when
+      the scheduler masks each rank down to ONE visible device
+      (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES per rank), LOCAL_RANK >= 1
+      maps to that device 0;
+    * ``ZF_DEVICE`` (explicit) overrides it — for ranks that share one GPU on
+      purpose (HostAllgather tests); with WORLD_SIZE > 1 that puts several
+      ranks on one device, so it warns;
+    * a LOCAL_RANK beyond the visible devices of a multi-device process
+      (oversubscribed launch) raises before any RCCL call would fail."""
+    zf_dev = env.get("ZF_DEVICE")
+    local = env.get("LOCAL_RANK")
+    if zf_dev is not None and zf_dev != "":
+        dev = int(zf_dev)
+        if local is not None and int(env.get("WORLD_SIZE", "1")) > 1:
+            import warnings
+
+            warnings.warn(f"zenflow_amd: ZF_DEVICE={dev} overrides LOCAL_RANK={local} in a "
+                          f"{env.get('WORLD_SIZE')}-rank job (ranks sharing one GPU)", RuntimeWarning, stacklevel=3)
+    else:
+        dev = int(local or "0")
+        if n == 1 and dev >= 1:
+            dev = 0  # one visible device per rank
+    if not 0 <= dev < n:
+        raise RuntimeError(
+            f"zenflow_amd: device {dev} (LOCAL_RANK/ZF_DEVICE) is not visible; "
+            f"{n} HIP device(s) visible — launch at most one rank per GPU"
+        )
+    return dev
+
+
 def ensure_device() -> None:
     """Fail loudly when no GPU is visible (no silent CPU path)."""
     global _device_ready
@@ -221,17 +254,7 @@ def ensure_device() -> None:
             "zenflow_amd: no HIP device is visible; the product path runs only on "
             "MI355X (gfx950) and has no CPU fallback."
         )
-    # ZF_DEVICE (explicit) wins over LOCAL_RANK (one rank per GPU); ranks
-    # that share one GPU on purpose (HostAllgather tests) set ZF_DEVICE
-    dev = int(os.environ.get("ZF_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-    n = device_count()
-    if not 0 <= dev < n:
-        # one process per GPU: an oversubscribed or mis-masked launch would put
-        # two ranks on one device and fail later inside RCCL
-        raise RuntimeError(
-            f"zenflow_amd: device {dev} (LOCAL_RANK/ZF_DEVICE) is not visible; "
-            f"{n} HIP device(s) visible — launch at most one rank per GPU"
-        )
+    dev = select_device(os.environ, device_count())
     check(load_library().zf_set_device(dev), "zf_set_device")
     _device_ready = True
 

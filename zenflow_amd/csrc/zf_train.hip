@@ -1494,15 +1494,19 @@ int zf_trainer_set_comm(zf_trainer_t* t, const zf_comm_desc* comm) {
   if (c.world < 1 || c.rank < 0 || c.rank >= c.world) return zf::einval("bad rank %d / world %d", c.rank, c.world);
   if (c.world > zf::kMaxLeaves) return zf::enotsup("training: more than 64 ranks");
   if (c.world > 1 && !c.allgather) return zf::einval("communicator without allgather");
-  ZF_TRY_HIP(hipDeviceSynchronize());
-  if (t->d_gath) (void)hipFree(t->d_gath);
-  t->d_gath = nullptr;
-  t->gath_bytes = 0;
-  if (c.world > 1) {
-    // largest exchange: the fp64 gradient of every rank
-    const int64_t per = std::max<int64_t>(t->nat_floats, 256) * (int64_t)sizeof(double);
-    t->gath_bytes = per * c.world;
-    ZF_TRY_HIP(hipMalloc(&t->d_gath, (size_t)t->gath_bytes));
+  // the gather buffer only grows (largest exchange: the fp64 gradient of
+  // every rank), and stays allocated while the communicator is cleared for a
+  // one-device step (train(): a batch with fewer rows than ranks, once per
+  // epoch), so clearing / restoring it costs no device sync or allocation
+  const int64_t need =
+      c.world > 1 ? std::max<int64_t>(t->nat_floats, 256) * (int64_t)sizeof(double) * c.world : 0;
+  if (need > t->gath_bytes) {
+    ZF_TRY_HIP(hipDeviceSynchronize());
+    if (t->d_gath) (void)hipFree(t->d_gath);
+    t->d_gath = nullptr;
+    t->gath_bytes = 0;
+    ZF_TRY_HIP(hipMalloc(&t->d_gath, (size_t)need));
+    t->gath_bytes = need;
   }
   t->comm = c;
   return ZF_OK;

@@ -12,12 +12,16 @@ unchanged.  The arithmetic itself always runs in the HIP kernels.
 from __future__ import annotations
 
 import copy
+import functools
+import inspect
+import itertools
 import threading
 from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import numpy as np
 
 _tls = threading.local()
+_serial = itertools.count(1)
 
 
 class Scope:
@@ -37,6 +41,12 @@ class Scope:
         self.initializing = initializing
         self.rng = rng  # numpy Generator while initializing
         self.path: Tuple[str, ...] = ()
+        # modules whose methods are running (innermost last), the per-call
+        # counters of inline submodules (flax compact naming: <Class>_<i> per
+        # parent), and this call's id (auto-names are re-derived per call)
+        self.stack: list = []
+        self.counters: Dict[Tuple[int, str], int] = {}
+        self.serial = next(_serial)
 
     def collection(self, name: str) -> Dict[str, Any]:
         return self.variables.get(name, {}) or {}
@@ -115,23 +125,108 @@ def current_scope() -> Scope:
     return s
 
 
+def _chain(module, owner):
+    """Attribute path from ``owner`` down to ``module``, or None when the
+    chain of ``_zf_parent`` / ``_zf_name`` links does not reach it."""
+    path = []
+    m = module
+    while m is not None and m is not owner:
+        name = m.__dict__.get("_zf_name")
+        if name is None:
+            return None
+        path.append(name)
+        m = m.__dict__.get("_zf_parent")
+    return None if m is None else list(reversed(path))
+
+
 def scope_for(module) -> Union[Scope, SubScope]:
     """The scope ``module`` sees: the root scope when it is the module that
-    ``apply``/``init`` was called on (or not a descendant of it), else the
-    sub-scope at its attribute path below that module — so a Flow held as
-    ``self.flow`` by an outer module reads ``variables[col]["flow"]``
-    (examples/deep_set.ipynb: ``self.flow(y, c, train=train)``)."""
+    ``apply``/``init`` was called on, else the sub-scope at its attribute
+    path below that module — so a Flow held as ``self.flow`` by an outer
+    module reads ``variables[col]["flow"]`` (examples/deep_set.ipynb:
+    ``self.flow(y, c, train=train)``).  A submodule created inline in a
+    method (``Phi()(x)``) or held where no attribute names it (a dict, a
+    ``_private`` attribute) is named ``<Class>_<i>`` after the module that
+    calls it, as flax.linen's compact methods name them; a module with no
+    link to the one ``apply``/``init`` runs on raises."""
     s = current_scope()
     if s.owner is None or module is s.owner:
         return s
-    path = []
-    m = module
-    while m is not None and m is not s.owner:
-        path.append(m.__dict__.get("_zf_name"))
-        m = m.__dict__.get("_zf_parent")
-    if m is None or any(p is None for p in path):
-        return s
-    return SubScope(s, reversed(path))
+    path = _chain(module, s.owner)
+    if path is None or (module.__dict__.get("_zf_auto") not in (None, s.serial)):
+        _adopt(s, module)
+        path = _chain(module, s.owner)
+    if path is None:
+        raise RuntimeError(
+            f"{type(module).__name__} is used inside {type(s.owner).__name__}.apply/init but is not one of its "
+            "submodules (assign it as an attribute, or create it inside the calling module's method)")
+    return SubScope(s, path)
+
+
+def _adopt(s: Scope, module) -> None:
+    """Name an unlinked ``module`` after the module whose method is running
+    (the caller): ``<Class>_<i>``, i counting that caller's inline children
+    of the class in this call (flax compact naming)."""
+    parent = next((m for m in reversed(s.stack) if m is not module), s.owner)
+    if parent is None:
+        return
+    cls = type(module).__name__
+    key = (id(parent), cls)
+    i = s.counters.get(key, 0)
+    s.counters[key] = i + 1
+    d = module.__dict__
+    d["_zf_parent"] = parent
+    d["_zf_name"] = f"{cls}_{i}"
+    d["_zf_auto"] = s.serial
+
+
+def _wrap_method(fn):
+    """A module method run under a scope: pushes the module on the scope's
+    call stack (so inline submodules it calls are named after it), names the
+    module itself if nothing links it to the scope's owner, and while
+    initializing creates the variables its setup() declared."""
+
+    @functools.wraps(fn)
+    def wrapped(self, *args, **kwargs):
+        s = getattr(_tls, "scope", None)
+        if s is None or (s.stack and s.stack[-1] is self):
+            return fn(self, *args, **kwargs)
+        if s.owner is not None and self is not s.owner:
+            if _chain(self, s.owner) is None or self.__dict__.get("_zf_auto") not in (None, s.serial):
+                _adopt(s, self)
+        s.stack.append(self)
+        try:
+            if s.initializing:
+                self._ensure_setup()
+                for name in list(self.__dict__.get("_zf_refs", {})):
+                    getattr(self, name)  # flax creates setup()'s variables at init
+            return fn(self, *args, **kwargs)
+        finally:
+            s.stack.pop()
+
+    wrapped._zf_wrapped = True
+    return wrapped
+
+
+_NOT_WRAPPED = {"init", "apply", "param", "variable", "setup", "bind"}
+
+
+class _SetupRef:
+    """What ``self.param`` / ``self.variable`` return inside ``setup()``: a
+    declaration, bound to the variables of whichever init/apply call reads
+    the attribute (flax re-runs setup per bind; here setup runs once and its
+    declarations resolve per call)."""
+
+    def __init__(self, kind, args):
+        self.kind, self.args = kind, args
+
+    def resolve(self, module):
+        if self.kind == "param":
+            return Module.param(module, *self.args)
+        return Module.variable(module, *self.args)
+
+    def __repr__(self):
+        return f"<{self.kind} {self.args[0]!r} declared in setup()>"
 
 
 def _resolve_method(module, method):
@@ -163,24 +258,43 @@ class Module:
     module's ``apply``/``init``.  ``param``/``variable`` give user modules
     their own variables."""
 
+    def __init_subclass__(cls, **kwargs):
+        super().__init_subclass__(**kwargs)
+        for name, fn in list(cls.__dict__.items()):
+            if (name.startswith("_") and name != "__call__") or name in _NOT_WRAPPED:
+                continue
+            if inspect.isfunction(fn) and not getattr(fn, "_zf_wrapped", False):
+                setattr(cls, name, _wrap_method(fn))
+
     def __setattr__(self, name, value):
+        if isinstance(value, _SetupRef):  # self.w = self.param(...) in setup()
+            self.__dict__.setdefault("_zf_refs", {})[name] = value
+            self.__dict__.pop(name, None)
+            return
         object.__setattr__(self, name, value)
         if not name.startswith("_"):
             _name_children(self, name, value)
 
     def __getattr__(self, name):
-        # flax runs setup() lazily on first attribute access
         d = self.__dict__
+        refs = d.get("_zf_refs")
+        if refs is not None and name in refs:  # a setup() declaration: this call's value
+            return refs[name].resolve(self)
+        # flax runs setup() lazily on first attribute access
         if not name.startswith("__") and not d.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
-            d["_zf_setup_done"] = True
-            self.setup()
+            self._ensure_setup()
             return getattr(self, name)
         raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
 
     def _ensure_setup(self) -> None:
-        if not self.__dict__.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
-            self.__dict__["_zf_setup_done"] = True
-            self.setup()
+        d = self.__dict__
+        if not d.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
+            d["_zf_setup_done"] = True
+            d["_zf_in_setup"] = True
+            try:
+                self.setup()
+            finally:
+                d["_zf_in_setup"] = False
 
     def init(self, rng, *args, method=None, **kwargs) -> Dict[str, Any]:
         """Create the variables (``params`` + ``batch_stats``) for the input shapes.
@@ -250,7 +364,11 @@ class Module:
     # variables of user modules (flax.linen.Module.param / .variable) ---------
     def param(self, name: str, init_fn: Callable, *init_args):
         """``params`` variable ``name`` of this module: created by
-        ``init_fn(rng, *init_args)`` while initializing, read otherwise."""
+        ``init_fn(rng, *init_args)`` while initializing, read otherwise.
+        Inside ``setup()`` it declares the variable: the attribute it is
+        assigned to reads the value of the current init/apply call."""
+        if self.__dict__.get("_zf_in_setup"):
+            return _SetupRef("param", (name, init_fn, *init_args))
         s = scope_for(self)
         cur = s.collection("params")
         if name not in cur:
@@ -262,6 +380,8 @@ class Module:
 
     def variable(self, col: str, name: str, init_fn: Callable, *init_args) -> "Variable":
         """A mutable variable of collection ``col`` (e.g. ``batch_stats``)."""
+        if self.__dict__.get("_zf_in_setup"):
+            return _SetupRef("variable", (col, name, init_fn, *init_args))
         s = scope_for(self)
         if name not in s.collection(col):
             if not s.initializing:
