@@ -107,9 +107,9 @@ int zf_normalize_spline_params(float* dx, float* dy, float* slope, int64_t M, in
 
 /* Activation of the conditioner's hidden layers (NSC.act, bijectors.py:319;
  * the flax.linen / jax.nn functions of those names).  Split-MFMA kernel
- * (zf_flow_kernel_variant): swish, relu, tanh, gelu, elu and leaky_relu on
- * the f16x2 scheme, sigmoid on bf16x3; softplus runs on the fp32 kernel.
- * The trainer takes all eight. */
+ * (zf_flow_kernel_variant): all eight on the f16x2 scheme (sigmoid and
+ * softplus centred on 1/2 and log 2); under ZF_X3_SCHEME=bf16x3 softplus
+ * runs on the fp32 kernel.  The trainer takes all eight. */
 #define ZF_ACT_SWISH 0      /* nn.swish = nn.silu: x * sigmoid(x) */
 #define ZF_ACT_RELU 1       /* nn.relu */
 #define ZF_ACT_TANH 2       /* nn.tanh */
@@ -179,11 +179,11 @@ int zf_flow_destroy(zf_flow_t* handle);
  * implementation detail made observable for tests and benchmarks):
  * ZF_KERNEL_FP32 (fp32 MFMA, any supported shape), or the split-MFMA kernel
  * for the shapes it covers (x3_eligible: every hidden width <= 256, one knot
- * count in {8, 16, 32} for all couplings, dim <= 64, no softplus coupling)
- * in one of two schemes: ZF_KERNEL_F16X2 (default: two-term fp16 split of
+ * count in {8, 16, 32} for all couplings, dim <= 64) in one of two
+ * schemes: ZF_KERNEL_F16X2 (default: two-term fp16 split of
  * power-of-two-scaled operands, three fp16 MFMAs per k-step) or
  * ZF_KERNEL_BF16X3 (three-term bf16 split, six bf16 MFMAs per k-step;
- * ZF_X3_SCHEME=bf16x3, or any flow with a sigmoid coupling).  The
+ * ZF_X3_SCHEME=bf16x3, where a softplus coupling runs on the fp32 kernel).  The
  * environment is read at zf_flow_create time; ZF_DISABLE_X3=1 forces
  * ZF_KERNEL_FP32.  -1 if h is NULL. */
 #define ZF_KERNEL_FP32 0

@@ -36,6 +36,13 @@ CONFIGS = {
     "d3k32": dict(D=3, C=0, K=32, layers=(128, 96), latent="beta"),
     "d4h256k8": dict(D=4, C=1, K=8, layers=(256, 256), latent="normal"),
     "d5h64": dict(D=5, C=0, K=16, layers=(64, 64), latent="normal"),
+    # knot counts between the instantiated 8 / 16 / 32: the split-MFMA kernel
+    # pads them with inert knots (x3_padded_knots; 15 -> 32, 7 -> 16)
+    "k12": dict(D=4, C=0, K=12, layers=(128, 128), latent="normal"),
+    "k5c1": dict(D=3, C=1, K=5, layers=(128, 128), latent="beta"),
+    "k15": dict(D=4, C=0, K=15, layers=(128, 128), latent="normal"),
+    "k24h256": dict(D=6, C=0, K=24, layers=(256, 256), latent="normal", couplings=3),
+    "k3": dict(D=2, C=0, K=3, layers=(64, 64), latent="normal"),
     # NeuralSplineCoupling(act=...) other than swish (bijectors.py:319): the
     # split-MFMA kernel's activation switch (sigmoid / softplus: the fp32
     # kernel) and the trainer

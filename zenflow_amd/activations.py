@@ -11,9 +11,10 @@ match the implemented form it names, or — without a known name — one of
 them (a warning says which); anything else raises NotImplementedError.
 
 Kernels (zf_flow_create picks them): the split-MFMA kernel
-runs swish (f16x2 slot schedule), relu / leaky_relu / tanh / gelu / elu
-(f16x2, ``OACT`` instantiation), sigmoid (bf16x3); softplus runs on the
-fp32-MFMA kernel.  The trainer takes all eight."""
+runs all eight on its f16x2 scheme — swish on its tuned form, relu /
+leaky_relu / tanh / gelu / elu through the ``OACT`` instantiation, sigmoid
+and softplus there too, centred on 1/2 and log 2.  The trainer takes all
+eight."""
 
 from __future__ import annotations
 

@@ -53,7 +53,8 @@ struct DevFlow {
   int HP, nslot, per_wave, x3_ok;
   int small_floats;  // packed blob [0, small_floats): per-op small parameters
   int x3_par_bytes;  // split-MFMA kernel: LDS bytes of one NSC's small-parameter region (max over NSCs)
-  int _pad[2];
+  int kreal;  // split-MFMA kernels: the couplings' knot count (the kernel's K may be padded above it)
+  int _pad;
   float lat_c0, lat_c1, lat_c2, lat_c3;
   DevOp ops[kMaxOps];
 };
@@ -255,15 +256,17 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
 // latent.log_prob(z) + log_det, nan_to_num (flow.py:41-48;
 // distributions.py:16-33), block partial of sum(log_prob) for the NLL, and
 // the optional y / log_det outputs.  Partials: block b writes part[b*pstride]
-// (and zero into the pstride-1 slots after it that are < nparts), so every
-// kernel shape leaves the same ceil(N/128)-entry workspace for reduce.
+// (and zero into the pstride-1 slots after it that are < nparts), or
+// part[slot] when given, so every kernel shape leaves the same
+// ceil(N/128)-entry workspace for reduce.
 template <int NW>
 __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, const float* xs, int s,
                                               int hh, int lane, int wave, int rot, int D, long long row,
                                               bool valid, float ld, float* __restrict__ lp_out,
                                               double* __restrict__ block_partial, int pstride,
                                               long long nparts, float* __restrict__ y_out,
-                                              float* __restrict__ ld_out, double* s_part) {
+                                              float* __restrict__ ld_out, double* s_part,
+                                              long long slot = -1) {
   if (lp_out != nullptr) {
     const int lt = F->latent;
     const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
@@ -308,7 +311,9 @@ __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, con
       if (threadIdx.x == 0) {
         double acc = 0.0;
         for (int w = 0; w < NW; ++w) acc += s_part[w];
-        const long long b0 = (long long)blockIdx.x * pstride;
+        // slot: the partial index of these rows when a block covers several
+        // 128-row slots (the two-set kernel calls this once per set)
+        const long long b0 = slot >= 0 ? slot : (long long)blockIdx.x * pstride;
         block_partial[b0] = acc;
         for (int k = 1; k < pstride; ++k)
           if (b0 + k < nparts) block_partial[b0 + k] = 0.0;
@@ -343,6 +348,11 @@ struct X3Launch {
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);
+// Two-set kernel (zf_flow_x4_kernel.h): small_pieces = KiB of small
+// parameters staged in LDS, ks0 = Dense_0 k-steps
+int launch_flow_x4(const X3Launch& a, bool inverse, int small_pieces, int ks0);
+bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0);
+size_t x4_lds_bytes_host(int K, bool one, int D, int C, int small_pieces);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 int x3_last_tiles(int K);
 int x3_pairs(const zf_flow_desc& desc);

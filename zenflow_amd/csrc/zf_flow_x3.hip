@@ -35,6 +35,9 @@ float bf16_f(uint16_t b) {
 
 }  // namespace
 
+int x3_padded_knots(int K);
+int x3_param_of(int jp, int Kp, int K, float* fill);
+
 // One knot count for all couplings and one of the instantiated shapes
 // (launch_flow_x3).
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
@@ -46,22 +49,80 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
     if (op.kind != ZF_OP_NSC) continue;
     // relu, leaky_relu, tanh, gelu and elu (act(0) = 0, |act(v)| <= |v|: the
     // f16x2 per-sample power-of-two scale keeps every value's relative
-    // precision) run on either scheme.  sigmoid carries its information as
-    // small deviations from 1/2, which f16x2's 22-bit split operands resolve
-    // worse than fp32 (1e-3 relative on tiny pre-activations amplified by
-    // large weights), so a flow with a sigmoid coupling runs the scaling-free
-    // bf16x3 scheme (x3_scheme_for).  softplus stays on the fp32 kernel: in
-    // the same regime (deviations from log 2 under 1e4-scale weights, a
-    // cancellation of 1e3-size products) bf16x3's mean error was 5x the
-    // fp32 oracle's, the fp32 kernel's equal to it (scripts/diag_acts.py).
-    if (op.act == ZF_ACT_SOFTPLUS) return false;
+    // precision) run on either scheme; sigmoid and softplus on f16x2 run
+    // centred (act(v) - C, C = 1/2 / log 2 folded into the next bias:
+    // act_tile_centered, x3_pack).  On bf16x3 (ZF_X3_SCHEME=bf16x3) sigmoid
+    // runs uncentred and softplus stays on the fp32 kernel: in the
+    // tiny-activation regime (deviations from log 2 under 1e4-scale weights,
+    // a cancellation of 1e3-size products) bf16x3's mean error was 5x the
+    // fp32 oracle's (scripts/diag_acts.py).
+    if (op.act == ZF_ACT_SOFTPLUS && x3_scheme() == 3) return false;
     if (K == 0) K = op.knots;
     if (op.knots != K) return false;
   }
   // hidden <= 128 runs padded to 128 (the caller pads HP); any dim the
   // fp32 kernel takes (LDS is checked at create time)
-  if (HP > 256 || desc.dim > 64 || !(K == 8 || K == 16 || K == 32)) return false;
-  *K_out = K;
+  const int Kp = x3_padded_knots(K);
+  if (HP > 256 || desc.dim > 64 || Kp == 0) return false;
+  *K_out = Kp;
+  return true;
+}
+
+// The instantiated knot count a flow of K knots runs at (0: none).  K < Kp
+// runs as Kp knots whose extra ones are inert (x3_param_of): their widths /
+// heights enter the sums as exact zeros (logit -2^40: squareplus = 0) and
+// their slope logits are 0 at the last real knot (the boundary derivative
+// 1) and NaN beyond, so the idx == K sliver still gives NaN (utils.py:
+// 224-230).  K = Kp - 1 is padded one size further: there the sliver bin
+// would be the instantiation's last, whose right slope is the boundary.
+int x3_padded_knots(int K) {
+  if (K < 2) return 0;
+  if (K <= 8 && K != 7) return 8;
+  if (K <= 16 && K != 15) return 16;
+  if (K <= 32 && K != 31) return 32;
+  return 0;
+}
+
+// Parameter jp (of 3 Kp - 1) of a padded (sample, dim) row -> the real
+// parameter of 3 K - 1 (widths, heights, slopes), or -1 with the inert
+// value in *fill.
+int x3_param_of(int jp, int Kp, int K, float* fill) {
+  if (jp < Kp) {
+    *fill = -1099511627776.0f;  // -2^40: x + sqrt(x^2 + 4) = 0 exactly
+    return jp < K ? jp : -1;
+  }
+  if (jp < 2 * Kp) {
+    *fill = -1099511627776.0f;
+    return jp - Kp < K ? K + (jp - Kp) : -1;
+  }
+  const int q = jp - 2 * Kp;
+  *fill = q == K - 1 ? 0.0f : __builtin_nanf("");
+  return q < K - 1 ? 2 * K + q : -1;
+}
+
+// The two-set kernel (flow_kernel_x4): f16x2, every coupling swish with two
+// hidden layers (width <= 128), at most 2 transformed dims, <= 4 conditioner
+// inputs, one knot count in {8, 16, 32}, only Rolls between couplings.
+// ZF_X4=0 keeps such flows on flow_kernel_x3 (A/B runs).
+bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0) {
+  const char* env = std::getenv("ZF_X4");
+  if (env && env[0] == '0') return false;
+  if (NT != 2 || oact || HP != 128 || desc.dim / 2 > 2 || desc.dim < 2) return false;
+  if (!(K == 16)) return false;  // instantiated knot counts
+  const int DC = desc.dim - desc.dim / 2 + desc.cond_dim;
+  if (DC > 4) return false;
+  int first = -1, last = -1;
+  for (int i = 0; i < desc.n_ops; ++i) {
+    const zf_op_desc& op = desc.ops[i];
+    if (op.kind != ZF_OP_NSC) continue;
+    if (op.n_hidden != 2 || op.act != ZF_ACT_SWISH) return false;
+    if (first < 0) first = i;
+    last = i;
+  }
+  if (first < 0) return false;
+  for (int i = first; i <= last; ++i)
+    if (desc.ops[i].kind != ZF_OP_NSC && desc.ops[i].kind != ZF_OP_ROLL) return false;
+  *ks0 = (DC + 1) / 2;
   return true;
 }
 
@@ -72,15 +133,11 @@ int x3_scheme() {
   return 2;
 }
 
-// The scheme of one flow: bf16x3 when asked for, or when a coupling's
-// activation is sigmoid (x3_eligible); f16x2 otherwise.
+// The scheme of one flow: bf16x3 when asked for (ZF_X3_SCHEME=bf16x3),
+// f16x2 otherwise (every activation; sigmoid / softplus centred).
 int x3_scheme_for(const zf_flow_desc& desc) {
-  if (x3_scheme() == 3) return 3;
-  for (int i = 0; i < desc.n_ops; ++i) {
-    const zf_op_desc& op = desc.ops[i];
-    if (op.kind == ZF_OP_NSC && op.act == ZF_ACT_SIGMOID) return 3;
-  }
-  return 2;
+  (void)desc;
+  return x3_scheme() == 3 ? 3 : 2;
 }
 
 int x3_last_tiles(int K) { return (3 * K - 1 + 15) / 16; }
@@ -106,7 +163,9 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
     const zf_op_desc& op = desc.ops[i];
     if (op.kind != ZF_OP_NSC) continue;
     DevOp& d = F.ops[i];
-    const int dt = desc.dim / 2, K = op.knots, S = 3 * K - 1;
+    // K: the coupling's knots; Kp: the instantiation's (x3_padded_knots)
+    const int dt = desc.dim / 2, K = x3_padded_knots(op.knots), S = 3 * K - 1;
+    const int Kr = op.knots, Sr = 3 * Kr - 1;
     const bool one = dt == 1;
     const int TL = one ? x3_last_tiles_one(K) : x3_last_tiles(K), NP = x3_pairs(desc);
     d.x3 = (long long)stream.size() * 2;
@@ -115,7 +174,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
     for (int l = 1; l <= op.n_hidden; ++l) {
       const bool last = (l == op.n_hidden);
       const int in = op.hidden[l - 1];
-      const int out = last ? dt * S : op.hidden[l];
+      const int out = last ? dt * Sr : op.hidden[l];
       const int NOUT = last ? TL : T;
       const float* W = nat + op.off_w[l];
       // f16x2: the inputs of swished layers' activations carry log2(e)
@@ -151,7 +210,9 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
                     const int h = (rho >> 2) & 1, r = (rho & 3) + 4 * (rho >> 3);
                     const int jp = one ? 32 * o + 16 * h + r : 16 * o + r;
                     const int dd = one ? 0 : 2 * pr + h;
-                    col = (dd < dt && jp < S) ? dd * S + jp : -1;
+                    float fill;
+                    const int jr = jp < S ? x3_param_of(jp, K, Kr, &fill) : -1;
+                    col = (dd < dt && jr >= 0) ? dd * Sr + jr : -1;
                   }
                   const float x = (k < in && col >= 0) ? W[(int64_t)k * out + col] : 0.f;
                   if (NT == 3) {
@@ -174,6 +235,37 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
               stream.insert(stream.end(), pp, pp + NT * 64 * 8);
             }
     }
+    // f16x2 sigmoid / softplus: the kernel feeds act(v) - C to every layer
+    // after Dense_0 (act_tile_centered), so each such layer's bias takes
+    // C * sum_k W[k][j] (fp64 sums, rounded once); the last layer's fold goes
+    // into the permuted last bias below
+    std::vector<double> lastfold;
+    if (NT == 2 && (op.act == ZF_ACT_SIGMOID || op.act == ZF_ACT_SOFTPLUS)) {
+      const double C = op.act == ZF_ACT_SIGMOID ? 0.5 : 0.69314718055994530942;
+      for (int l = 1; l <= op.n_hidden; ++l) {
+        const bool last = l == op.n_hidden;
+        const int in = op.hidden[l - 1];
+        const int out = last ? dt * Sr : op.hidden[l];
+        const float* W = nat + op.off_w[l];
+        std::vector<double> cs(out, 0.0);
+        for (int k = 0; k < in; ++k)
+          for (int j = 0; j < out; ++j) cs[j] += (double)W[(int64_t)k * out + j];
+        if (last) {
+          for (double& v : cs) v *= C;
+          lastfold.swap(cs);
+          continue;
+        }
+        for (int o = 0; o < T; ++o)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int r = 0; r < 16; ++r) {
+              const int ii = 32 * o + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              if (ii < out) {
+                float& b = packed[d.b[l] + (o * 2 + hh) * 16 + r];
+                b = (float)((double)b + C * cs[ii]);
+              }
+            }
+      }
+    }
     // f16x2: Dense_0 (fp32 fragments, d.w[0]) and the hidden biases of the
     // swished layers join the log2(e) prescale (act_swish); other
     // activations take their pre-activations unscaled.
@@ -192,7 +284,14 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
         for (int h = 0; h < 2; ++h)
           for (int r = 0; r < 16; ++r) {
             const int jp = one ? 32 * o + 16 * h + r : 16 * o + r, dd = one ? 0 : 2 * pr + h;
-            packed[d.x3_blast + ((pr * TL + o) * 2 + h) * 16 + r] = (dd < dt && jp < S) ? B[dd * S + jp] : 0.f;
+            float fill = 0.f;
+            const int jr = (dd < dt && jp < S) ? x3_param_of(jp, K, Kr, &fill) : -1;
+            float b = 0.f;
+            if (jr >= 0)
+              b = lastfold.empty() ? B[dd * Sr + jr] : (float)((double)B[dd * Sr + jr] + lastfold[dd * Sr + jr]);
+            else if (dd < dt && jp < S)
+              b = fill;  // inert padding knot
+            packed[d.x3_blast + ((pr * TL + o) * 2 + h) * 16 + r] = b;
           }
   }
   // next-NSC copies (x3_npieces above held each op's own group-0 pieces)

@@ -225,6 +225,41 @@ __device__ __forceinline__ void act_tile_fixed(floatx16& t, float c) {
   for (int r = 0; r < 16; ++r) t[r] = act_other(CODE, t[r]) * c;
 }
 
+// f16x2 sigmoid / softplus, centred: their information
+// sits in small deviations from 1/2 and log 2, which a per-sample scale of
+// the raw value cannot resolve to fp32's precision.  The kernel feeds
+// a(v) = act(v) - C to the split MFMA (C = 1/2, log 2; a(0) = 0 and
+// |a(v)| <= |v|, so x3_act_scale's per-sample scale keeps a's relative
+// precision), and x3_pack folds C * colsum(W) of the consuming layer into
+// its bias.  act(v) is rounded to fp32 first, as the reference's
+// jax.nn.sigmoid / softplus output is, so a = fl(act(v)) - C carries the
+// reference's own rounding (the subtraction is exact for act(v) in [C/2, 2C]).
+constexpr float kLn2 = 0.693147180559945309f;
+__device__ __forceinline__ float act_sigmoid_centered(float v) {
+  // 1 / (1 + 2^(-v log2 e)) with a residual-corrected reciprocal (as the
+  // bf16x3 form); 1 + e = inf (v < -88) gives 0
+  const float d = 1.0f + __builtin_amdgcn_exp2f(-v * kSwishPrescale);
+  const float q = __builtin_amdgcn_rcpf(d);
+  const float sg = __builtin_fmaf(q, __builtin_fmaf(-d, q, 1.0f), q);
+  return (d == __builtin_huge_valf() ? 0.0f : sg) - 0.5f;
+}
+__device__ __forceinline__ float act_softplus_centered(float v) {
+  // logaddexp(v, 0) = max(v, 0) + log1p(exp(-|v|)): log1p from the hardware
+  // log2 of 1 + t, or its series below t = 1/64 (where 1 + t loses t's bits)
+  const float t = __builtin_amdgcn_exp2f(-fabsf(v) * kSwishPrescale);
+  const float lg = __builtin_amdgcn_logf(1.0f + t) * kLn2;
+  const float ser = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, -0.25f, 1.0f / 3.0f), -0.5f), 1.0f);
+  const float sp = fmaxf(v, 0.0f) + (t < 0.015625f ? ser : lg);
+  return (v != v ? v : sp) - kLn2;
+}
+
+template <int CODE>
+__device__ __forceinline__ void act_tile_centered(floatx16& t, float c) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    t[r] = (CODE == ZF_ACT_SIGMOID ? act_sigmoid_centered(t[r]) : act_softplus_centered(t[r])) * c;
+}
+
 template <int CODE>
 __device__ __forceinline__ void act_tile_plain(floatx16& t) {
 #pragma unroll
@@ -271,6 +306,8 @@ __device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
       case ZF_ACT_GELU: act_tile_fixed<ZF_ACT_GELU>(t, c); break;
       case ZF_ACT_ELU: act_tile_fixed<ZF_ACT_ELU>(t, c); break;
       case ZF_ACT_LEAKY_RELU: act_tile_fixed<ZF_ACT_LEAKY_RELU>(t, c); break;
+      case ZF_ACT_SIGMOID: act_tile_centered<ZF_ACT_SIGMOID>(t, c); break;
+      case ZF_ACT_SOFTPLUS: act_tile_centered<ZF_ACT_SOFTPLUS>(t, c); break;
       default:
 #pragma unroll
         for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
@@ -328,7 +365,8 @@ __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, fl
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
   m = fmaxf(m, __shfl_xor(m, 32));
   // OACT: |act(v)| <= |v| for every activation the kernel takes (relu,
-  // leaky_relu, tanh, gelu, elu; x3_eligible), so the bound holds as for swish.
+  // leaky_relu, tanh, gelu, elu, and sigmoid / softplus centred:
+  // act_tile_centered), so the bound holds as for swish.
   // (e clamped: a layer input below 2^-60 keeps scale 2^74, so a bias
   // seeded as bias / us stays finite)
   const int e = max(__builtin_amdgcn_frexp_expf(m), -60);
@@ -1083,7 +1121,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   }
   int nsc_i = 0;  // NSCs entered, in execution order: parameter region nsc_i & 1
 
-  const KnotConsts kc(K);
+  const KnotConsts kc(F->kreal);  // the couplings' knots (K may be padded above them)
   const int nq = op_end - op_begin;
   for (int q = 0; q < nq; ++q) {
     const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
