@@ -25,3 +25,9 @@ for c in ${ACT_CONFIGS:-cfg2sigmoid cfg2softplus cfg2relu}; do
   timeout -k 10 200 python bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline --no-spline-kernel > gpurun_out/x4/b_$c.log 2>&1 || { tail -5 gpurun_out/x4/b_$c.log; exit 1; }
   python -c "import json; d=json.loads([l for l in open('gpurun_out/x4/b_$c.log') if l.startswith('{')][-1]); print('$c', round(d['value']/1e6,1), 'M/s', d['config'].get('kernel'))"
 done
+for r in 1 2; do
+  for v in 0 1; do
+    ZF_K1_STREAM=$v timeout -k 10 120 python scripts/bench_rqs.py 20 16 > gpurun_out/x4/k1_$v.json || exit 1
+    python -c "import json; d=json.load(open('gpurun_out/x4/k1_$v.json')); print('K1 K=16 stream=$v', {k: (round(d[k]['frac'], 3), round(d[k]['us'], 1)) for k in ('forward', 'inverse', 'normalize') if k in d}, d.get('check'))"
+  done
+done

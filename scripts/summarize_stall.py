@@ -15,6 +15,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+KNAME = __import__("os").environ.get("ZF_STALL_KERNEL", "flow_kernel_x3")
 NCOUP = {"cfg2": 4, "cfg3": 4, "cfg3s": 4, "cfg4": 2, "cfg5": 8, "d8": 8, "cfg1": 2}  # NSC couplings per flow
 
 
@@ -25,7 +26,7 @@ def main(tag="r02", src=ROOT / "gpurun_out", prefix="pmc_st", label="cfg2"):
     kname = None
     for path in glob.glob(str(Path(src) / f"{prefix}*" / "run_counter_collection.csv")):
         for r in csv.DictReader(open(path)):
-            if "flow_kernel_x3" not in r["Kernel_Name"]:
+            if KNAME not in r["Kernel_Name"]:
                 continue
             if int(r.get("Grid_Size") or r["Grid_Size_X"]) < (1 << 20):
                 continue
@@ -36,7 +37,7 @@ def main(tag="r02", src=ROOT / "gpurun_out", prefix="pmc_st", label="cfg2"):
     simd = 1024 * cyc
     waves = med["SQ_WAVE_CYCLES"]
     out = {
-        "kernel": (kname[kname.index("flow_kernel_x3"):kname.index(">") + 1] if kname else "flow_kernel_x3")
+        "kernel": (kname[kname.index(KNAME):kname.index(">") + 1] if kname else KNAME)
         + f" ({label}), 2^20-row launches",
         "counters_median": med,
         "kernel_cycles": cyc,

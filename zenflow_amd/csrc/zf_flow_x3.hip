@@ -103,12 +103,13 @@ int x3_param_of(int jp, int Kp, int K, float* fill) {
 // The two-set kernel (flow_kernel_x4): f16x2, every coupling swish with two
 // hidden layers (width <= 128), at most 2 transformed dims, <= 4 conditioner
 // inputs, one knot count in {8, 16, 32}, only Rolls between couplings.
-// ZF_X4=0 keeps such flows on flow_kernel_x3 (A/B runs).
+// Opt-in (ZF_X4=1): measured slower than flow_kernel_x3.
 bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0) {
   const char* env = std::getenv("ZF_X4");
-  if (env && env[0] == '0') return false;
+  if (!(env && env[0] == '1')) return false;
   if (NT != 2 || oact || HP != 128 || desc.dim / 2 > 2 || desc.dim < 2) return false;
-  if (!(K == 16)) return false;  // instantiated knot counts
+  // instantiated knot counts (K = 32 with two transformed dims spills)
+  if (!(K == 8 || K == 16 || (K == 32 && desc.dim / 2 == 1))) return false;
   const int DC = desc.dim - desc.dim / 2 + desc.cond_dim;
   if (DC > 4) return false;
   int first = -1, last = -1;

@@ -234,23 +234,37 @@ __device__ __forceinline__ void act_tile_fixed(floatx16& t, float c) {
 // its bias.  act(v) is rounded to fp32 first, as the reference's
 // jax.nn.sigmoid / softplus output is, so a = fl(act(v)) - C carries the
 // reference's own rounding (the subtraction is exact for act(v) in [C/2, 2C]).
+// Near v = 0 both are evaluated from their series (|v| < 1/4: truncation
+// below 1e-9 of a), so a carries the deviation to fp32's relative precision
+// instead of the 1-2 ulp of 1/2 or log 2 the rounded act(v) carries there
+// (tiny pre-activations under large weights: the hardware log2 alone put
+// softplus' mean error at 2.3x the fp32 oracle's).
 constexpr float kLn2 = 0.693147180559945309f;
 __device__ __forceinline__ float act_sigmoid_centered(float v) {
   // 1 / (1 + 2^(-v log2 e)) with a residual-corrected reciprocal (as the
-  // bf16x3 form); 1 + e = inf (v < -88) gives 0
+  // bf16x3 form); 1 + e = inf (v < -88) gives 0.  |v| < 1/4: tanh(v/2)/2 =
+  // v/4 - v^3/48 + v^5/480 - 17 v^7/80640
   const float d = 1.0f + __builtin_amdgcn_exp2f(-v * kSwishPrescale);
   const float q = __builtin_amdgcn_rcpf(d);
   const float sg = __builtin_fmaf(q, __builtin_fmaf(-d, q, 1.0f), q);
-  return (d == __builtin_huge_valf() ? 0.0f : sg) - 0.5f;
+  const float v2 = v * v;
+  const float ser =
+      v * __builtin_fmaf(v2, __builtin_fmaf(v2, __builtin_fmaf(v2, -17.0f / 80640.0f, 1.0f / 480.0f), -1.0f / 48.0f),
+                         0.25f);
+  return fabsf(v) < 0.25f ? ser : (d == __builtin_huge_valf() ? 0.0f : sg) - 0.5f;
 }
 __device__ __forceinline__ float act_softplus_centered(float v) {
   // logaddexp(v, 0) = max(v, 0) + log1p(exp(-|v|)): log1p from the hardware
-  // log2 of 1 + t, or its series below t = 1/64 (where 1 + t loses t's bits)
+  // log2 of 1 + t, or its series below t = 1/64 (where 1 + t loses t's bits).
+  // |v| < 1/4: softplus(v) - log 2 = v/2 + v^2/8 - v^4/192 + v^6/2880
   const float t = __builtin_amdgcn_exp2f(-fabsf(v) * kSwishPrescale);
   const float lg = __builtin_amdgcn_logf(1.0f + t) * kLn2;
-  const float ser = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, -0.25f, 1.0f / 3.0f), -0.5f), 1.0f);
-  const float sp = fmaxf(v, 0.0f) + (t < 0.015625f ? ser : lg);
-  return (v != v ? v : sp) - kLn2;
+  const float ls = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, -0.25f, 1.0f / 3.0f), -0.5f), 1.0f);
+  const float sp = fmaxf(v, 0.0f) + (t < 0.015625f ? ls : lg);
+  const float v2 = v * v;
+  const float ser = v * __builtin_fmaf(v, __builtin_fmaf(v2, __builtin_fmaf(v2, 1.0f / 2880.0f, -1.0f / 192.0f), 0.125f),
+                                       0.5f);
+  return fabsf(v) < 0.25f ? ser : (v != v ? v : sp - kLn2);
 }
 
 template <int CODE>
@@ -1016,6 +1030,32 @@ __device__ __forceinline__ void x3_forward_eval(float x, const RqsBin& b, float&
   ld = b.oob ? 0.0f : l;                                           // :138
 }
 
+// The activation-switch kernels (OACT: relu ... softplus) take squareplus
+// with a correctly rounded square root (rsq + one residual step), as the
+// reference's fp32 jnp.sqrt: unbounded activations under large weights
+// (softplus, tiny-activation regime) drive the last layer's logits to
+// -5e3, where x + sqrt(x^2 + 4) cancels to the square root's last bit and a
+// 1-ulp hardware sqrt doubles the reference's rounding there (mean error
+// 1.7x the fp32 oracle's; with this form the CPU emulation of the kernel's
+// arithmetic gives 1.1x).  The swish kernels keep the hardware form (-4
+// VALU per parameter; their bounded-magnitude tests are at the oracle's level).
+__device__ __forceinline__ float x3_sqrt_cr(float a) {
+  const float y = __builtin_amdgcn_rsqf(a);
+  const float sq = a * y;
+  const float r = __builtin_fmaf(__builtin_fmaf(-sq, sq, a), 0.5f * y, sq);
+  return a == __builtin_huge_valf() ? a : r;  // x^2 + 4 = inf: sqrt = inf, as jnp.sqrt
+}
+template <bool CR>
+__device__ __forceinline__ float x3_squareplus2_t(float x) {
+  const float a = __builtin_fmaf(x, x, 4.0f);
+  return x + (CR ? x3_sqrt_cr(a) : __builtin_amdgcn_sqrtf(a));
+}
+template <bool CR>
+__device__ __forceinline__ float x3_squareplus_t(float x) {
+  const float a = __builtin_fmaf(x, x, 4.0f);
+  return 0.5f * (x + (CR ? x3_sqrt_cr(a) : __builtin_amdgcn_sqrtf(a)));
+}
+
 // Block: 4 waves x 32 samples, one 32-row input tile per weight group,
 // double-buffered in LDS.  Small parameters (BatchNorm, first Dense, biases,
 // ShiftBounds rows) are read from global memory (L2-resident), so the LDS
@@ -1296,12 +1336,24 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         }
         if constexpr (T == 4) __builtin_amdgcn_s_setprio(0);
         X3T(4);
+        // ONE at K = 16: tile 0 holds the widths on lane half 0 and the
+        // heights on half 1, so each half normalises its own 16 (squareplus,
+        // sum in order, quotients: the same operations per value) and one
+        // exchange per knot gives both halves both; tile 1's slopes (half 0)
+        // go to both halves.  Other ONE shapes exchange the whole row first.
+        constexpr bool kSplitWH = ONE && K == 16;
         float P[NPV];
 #pragma unroll
         for (int o = 0; o < TL; ++o)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            if constexpr (ONE) {  // both halves end up with all of the dim's parameters
+            if constexpr (kSplitWH) {
+              if (o == 0) P[r] = pa[0][r];
+              else {  // slope r of half 0, on both halves
+                const float other = __shfl_xor(pa[1][r], 32);
+                P[2 * K + r] = hh == 0 ? pa[1][r] : other;
+              }
+            } else if constexpr (ONE) {  // both halves end up with all of the dim's parameters
               const float other = __shfl_xor(pa[o][r], 32);
               P[32 * o + r] = hh == 0 ? pa[o][r] : other;
               P[32 * o + 16 + r] = hh == 0 ? other : pa[o][r];
@@ -1315,24 +1367,41 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         float ldv = 0.f;
         {
           float w[K], hg[K];
-          float sx = 0.f, sy = 0.f;
-#pragma unroll
-          for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-            w[j] = x3_squareplus2(P[j]);
-            hg[j] = x3_squareplus2(P[K + j]);
-            sx = sx + w[j];
-            sy = sy + hg[j];
-          }
-          // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
-          // 2*squareplus: the same quotient bits): the parameters
-          // themselves already differ from the reference's in the last ulp
-          // (GEMM summation order), so correctly rounded divisions buy nothing.
-          const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
           const float bc = kc.c * kc.rnorm;
+          if constexpr (kSplitWH) {
+            float sw = 0.f;  // half 0: the widths' sum, half 1: the heights'
 #pragma unroll
-          for (int j = 0; j < K; ++j) {
-            w[j] = __builtin_fmaf(w[j], ax, bc);
-            hg[j] = __builtin_fmaf(hg[j], ay, bc);
+            for (int j = 0; j < K; ++j) {
+              w[j] = x3_squareplus2_t<OACT>(P[j]);
+              sw = sw + w[j];
+            }
+            const float a = rcp_refined(sw) * kc.rnorm;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const float f = __builtin_fmaf(w[j], a, bc);
+              const float other = __shfl_xor(f, 32);
+              w[j] = hh == 0 ? f : other;
+              hg[j] = hh == 0 ? other : f;
+            }
+          } else {
+            float sx = 0.f, sy = 0.f;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
+              w[j] = x3_squareplus2_t<OACT>(P[j]);
+              hg[j] = x3_squareplus2_t<OACT>(P[K + j]);
+              sx = sx + w[j];
+              sy = sy + hg[j];
+            }
+            // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
+            // 2*squareplus: the same quotient bits): the parameters
+            // themselves already differ from the reference's in the last ulp
+            // (GEMM summation order), so correctly rounded divisions buy nothing.
+            const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              w[j] = __builtin_fmaf(w[j], ax, bc);
+              hg[j] = __builtin_fmaf(hg[j], ay, bc);
+            }
           }
           float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
@@ -1340,7 +1409,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           float* xp = xs + wrap((dact ? d : 0) + rot, D) * 32 + s;
           const float xv = *xp;
           const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
-                                                       [](float v) { return v == 0.f ? 1.f : x3_squareplus(v); });
+                                                       [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); });
           float yv;
           if (!INV) {
             float l;

@@ -30,8 +30,9 @@
 // permuted last bias, ShiftBounds rows) stay in LDS for the whole launch.
 //
 // Shapes: f16x2, every coupling swish with two hidden layers of width <= 128
-// (T = 4), at most 2 transformed dims (no dim-pair loop), knots 8 / 16 / 32,
-// conditioner inputs <= 4 (KS0 <= 2), only Rolls between couplings — every
+// (T = 4), at most 2 transformed dims (no dim-pair loop), knots 8 / 16 (32:
+// one transformed dim), conditioner inputs <= 4 (KS0 <= 2), only Rolls
+// between couplings — every
 // BASELINE config at hidden 128 (cfg1-cfg4) and the reference defaults at
 // dim 2-5 (x4_eligible, zf_flow_x3.hip).  Rows: block b holds rows
 // [256 b, 256 b + 256): set S of wave w the 32 rows 256 b + 128 S + 32 w +
@@ -41,6 +42,10 @@
 
 namespace zf {
 namespace {
+
+#ifndef X4_ABL
+#define X4_ABL 0  // tuning-only ablations (wrong results), never set in the shipped build
+#endif
 
 constexpr int kX4Waves = 4;                    // one wave per SIMD
 constexpr int kX4Rows = kX4Waves * 2 * kTile;  // 256 rows per block
@@ -108,9 +113,10 @@ __device__ __forceinline__ void x4_pin(const halfx8& x) { asm volatile("" ::"v"(
 
 __device__ __forceinline__ float x4_lanes_max(float m) {
   // lanes l and l ^ 32 hold the same sample: v_permlane32_swap gives each
-  // half the other's value in one instruction
+  // half the other's value in one instruction; m >= 0 (a max of |v|), so
+  // the larger bit pattern is the larger float (no NaN canonicalisation)
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return __uint_as_float(r[0] > r[1] ? r[0] : r[1]);
 }
 
 // x for the lower / upper lane half: {value of half 0, value of half 1} on
@@ -128,7 +134,11 @@ template <int K, bool ONE, bool INV, int KS0, int TL, bool VSPL, bool VL0>
 struct X4Stages {
   static constexpr int nFIN = VSPL ? 4 * TL : 0;  // finish: 4 values of one last-layer tile each
   static constexpr int nSPW = VSPL ? K : 0;       // squareplus of the widths (+ running sum)
-  static constexpr int nSPH = VSPL ? K : 0;       // heights
+  // ONE at K = 16: the widths sit on lane half 0 and the heights on half 1
+  // (tile 0), so each half normalises its own 16 and one exchange per knot
+  // gives both halves both (SPW covers both, no SPH)
+  static constexpr bool kSplitWH = ONE && K == 16;
+  static constexpr int nSPH = (VSPL && !kSplitWH) ? K : 0;  // heights
   static constexpr int nNR0 = VSPL ? 1 : 0;       // the two normalisers
   static constexpr int nNRM = VSPL ? K : 0;       // normalised widths / heights
   static constexpr int nBS0 = VSPL ? 1 : 0;       // bin-search start
@@ -202,7 +212,16 @@ __device__ __forceinline__ void x4_vstage(const X4Ctx& cx, X4Set<TL>& V, X4V<K, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float f = __builtin_fmaf(V.pa[o][4 * r4 + i], V.lus, v.bq[q % 3][i]);
-      if constexpr (ONE) {
+      if constexpr (St::kSplitWH) {
+        if constexpr (o == 0) {  // widths (half 0) / heights (half 1): normalised per half first
+          V.pa[0][4 * r4 + i] = f;
+          x4_pin(f);
+        } else {  // slopes (half 0) to both halves
+          float h1;
+          x4_halves(f, v.P[32 + 4 * r4 + i], h1);
+          x4_pin(v.P[32 + 4 * r4 + i]);
+        }
+      } else if constexpr (ONE) {
         // both halves get the whole row (tile o, half h, register r =
         // parameter 32 o + 16 h + r)
         x4_halves(f, v.P[32 * o + 4 * r4 + i], v.P[32 * o + 16 + 4 * r4 + i]);
@@ -213,6 +232,13 @@ __device__ __forceinline__ void x4_vstage(const X4Ctx& cx, X4Set<TL>& V, X4V<K, 
         x4_pin(f);
       }
     }
+  } else if constexpr (I >= St::oSPW && I < St::oSPW + St::nSPW && St::kSplitWH) {
+    // half 0: width j, half 1: height j; the running sum is sx on half 0, sy on half 1
+    constexpr int j = I - St::oSPW;
+    v.w[j] = x3_squareplus2(V.pa[0][j]);
+    v.sx = j == 0 ? v.w[0] : v.sx + v.w[j];
+    x4_pin(v.w[j]);
+    x4_pin(v.sx);
   } else if constexpr (I >= St::oSPW && I < St::oSPW + St::nSPW) {
     constexpr int j = I - St::oSPW;
     v.w[j] = x3_squareplus2(x4_P<K, ONE, TL, j>(V, v));
@@ -227,13 +253,20 @@ __device__ __forceinline__ void x4_vstage(const X4Ctx& cx, X4Set<TL>& V, X4V<K, 
     x4_pin(v.sy);
   } else if constexpr (I == St::oNR0 && VSPL) {
     v.ax = rcp_refined(v.sx) * cx.rnorm;
-    v.ay = rcp_refined(v.sy) * cx.rnorm;
+    if constexpr (!St::kSplitWH) v.ay = rcp_refined(v.sy) * cx.rnorm;
     v.bc = cx.cnorm * cx.rnorm;
     x4_pin(v.ax);
-    x4_pin(v.ay);
+    if constexpr (!St::kSplitWH) x4_pin(v.ay);
     // this lane's x (two dims: dim hh; ONE: dim 0 on both halves)
     v.xp = V.xs + wrap((ONE ? 0 : cx.hh) + V.rot, cx.D) * 32 + cx.s;
     v.xv = *v.xp;
+  } else if constexpr (I >= St::oNRM && I < St::oNRM + St::nNRM && St::kSplitWH) {
+    // normalise on the owning half, then the exchange: width j and height j on both halves
+    constexpr int j = I - St::oNRM;
+    const float f = __builtin_fmaf(v.w[j], v.ax, v.bc);
+    x4_halves(f, v.w[j], v.hg[j]);
+    x4_pin(v.w[j]);
+    x4_pin(v.hg[j]);
   } else if constexpr (I >= St::oNRM && I < St::oNRM + St::nNRM) {
     constexpr int j = I - St::oNRM;
     v.w[j] = __builtin_fmaf(v.w[j], v.ax, v.bc);
@@ -448,11 +481,19 @@ __device__ __forceinline__ void x4_slot(const char* lb, floatx16 (&hb)[4], float
                                         uint32_t (&csh)[4], float c, const X4Ctx& cx, X4Set<TL>& V, X4V<K, TL>& v,
                                         const X4VC& vc) {
   constexpr int t = m / 3, j = m % 3, ks = t / NOUT, o = t % NOUT;
+#if X4_ABL != 3  // tuning ablation 3: one A fragment per group step (wrong results)
   if constexpr (j == 0 && t + 1 < 2 * NOUT) load_frag<2>(lb + (((t + 1) * 2) << 10), fr[(t + 1) & 1]);
+#else
+  if constexpr (j == 0 && t == 0) { fr[1][0] = fr[0][0]; fr[1][1] = fr[0][1]; }
+#endif
   if constexpr (ks == 0) acc[o] = mfma_term2(fr[t & 1], cs, j, acc[o]);
   else acc[o] = mfma_term2(fr[t & 1], s1, j, acc[o]);
+#if X4_ABL != 4  // tuning ablation 4: no M-set VALU in the slots (wrong results)
   x3_valu_slot<4, NOUT, Q, m>(hb, cs, s1, tq, s1h, csh, c);
+#endif
+#if X4_ABL != 1  // tuning ablation 1: no V chunk in the phases (wrong results)
   x4_vrange<VB, VE, K, ONE, INV, KS0, TL, VSPL, VL0>(cx, V, v, vc);
+#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -474,8 +515,10 @@ template <int NOUT, int Q, int G0, int NS, int K, bool ONE, bool INV, int KS0, i
 __device__ __forceinline__ void x4_step(const char* __restrict__ x3, X4Pipe& p, const X4MC& mc, int g,
                                         floatx16 (&hb)[4], floatx16 (&acc)[NOUT], halfx8 (&cs)[2], float c,
                                         const X4Ctx& cx, X4Set<TL>& V, X4V<K, TL>& v, const X4VC& vc) {
+#if X4_ABL != 2  // tuning ablation 2: no per-group DMA wait / barrier (wrong results)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#endif
   x4_issue_next<TL>(x3, p, mc, g);
   const char* lb = p.cur + p.lane * 16;
   halfx8 fr[2][2];
