@@ -123,7 +123,9 @@ def _get(tree, path):
 
 GRAD_CASES = CASES + [("cfg1", 1024, 66), ("d8", 512, 67), ("d2h256", 256, 68), ("odd", 300, 69),
                       ("relu", 256, 70), ("gelu", 256, 71), ("tanh", 256, 72), ("softplus", 256, 73),
-                      ("sigmoid", 256, 74), ("elu", 256, 75), ("leaky_relu", 256, 76), ("mixed", 256, 77)]
+                      ("sigmoid", 256, 74), ("elu", 256, 75), ("leaky_relu", 256, 76), ("mixed", 256, 77),
+                      # a batch whose forward Dense layers run the bf16x3 split-MFMA GEMM (>= 512 128x128 tiles)
+                      ("cfg2", 65536, 79), ("cfg5", 32768, 78)]
 
 
 @pytest.mark.parametrize("name,N,seed", GRAD_CASES)
@@ -279,3 +281,35 @@ def test_split_set_gemm_matches_single_kernel(name, N, seed, monkeypatch):
     assert np.array_equal(out[0][1], out[1][1]), f"{np.sum(out[0][1] != out[1][1])} gradient entries differ"
     assert out[0][2] == out[1][2]
     assert np.array_equal(out[0][3], out[1][3], equal_nan=True)
+
+
+@pytest.mark.parametrize("name,N,seed", [("cfg2", 65536, 80), ("d2h256", 65536, 81)])
+def test_train_x3_gemm_matches_fp32_gemm(name, N, seed, monkeypatch):
+    """Large batches run the forward Dense layers on the bf16x3 split-MFMA
+    GEMM (gemm_x3_kernel): loss and every gradient element within 1e-5 of
+    the tensor's scale of the fp32-MFMA GEMM's (ZF_TRAIN_X3=0) — two fp32
+    evaluations of the same sums in different orders.  (Deeper flows, whose
+    gradients amplify a forward rounding difference further, are held to
+    float64 autograd with their conditioning instead: cfg5 in GRAD_CASES.)"""
+    case, flow, tr = _setup(name, N, seed)
+    loss_x3, g_x3 = tr.loss_grad(case["x"], case["c"])
+    monkeypatch.setenv("ZF_TRAIN_X3", "0")
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, sys; sys.path.insert(0, '.');"
+        "from tests.test_gpu_train import _setup;"
+        f"case, flow, tr = _setup({name!r}, {N}, {seed});"
+        "l, g = tr.loss_grad(case['x'], case['c']);"
+        "np.savez(sys.argv[1], l=np.float64(l), g=g)")
+    from pathlib import Path
+    import tempfile
+    root = Path(__file__).resolve().parents[1]
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "ref.npz"
+        subprocess.run([sys.executable, "-c", code, str(out)], cwd=root, check=True, timeout=300)
+        ref = np.load(out)
+        loss_32, g_32 = float(ref["l"]), ref["g"]
+    assert abs(loss_x3 - loss_32) <= 1e-5 * max(1.0, abs(loss_32))
+    scale = np.abs(g_32).max()
+    assert np.abs(g_x3 - g_32).max() <= 1e-5 * scale, np.abs(g_x3 - g_32).max() / scale

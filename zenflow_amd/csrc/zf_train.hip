@@ -73,6 +73,40 @@ __device__ __forceinline__ void gemm_epilogue(float v, int n, long long o, float
   C[o] = v;
 }
 
+// The same for four consecutive columns n..n+3 (n % 4 == 0 < N, N % 4 == 0,
+// 16-B aligned rows): one dwordx4 per array instead of four dword stores.
+__device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, float* __restrict__ C, int epi,
+                                               const float* __restrict__ bias, float* __restrict__ H,
+                                               const float* __restrict__ Z, int act) {
+  float x[4] = {v.x, v.y, v.z, v.w};
+  if (epi == kEpiBias) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + n);
+    x[0] = x[0] + b.x;
+    x[1] = x[1] + b.y;
+    x[2] = x[2] + b.z;
+    x[3] = x[3] + b.w;
+    if (H) {
+      float y[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) y[t] = act == ZF_ACT_SWISH ? x[t] * sigmoidf(x[t]) : act_other(act, x[t]);
+      *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+    }
+  } else if (epi == kEpiDSwish) {
+    const float4 z4 = *reinterpret_cast<const float4*>(Z + o);
+    const float z[4] = {z4.x, z4.y, z4.z, z4.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (act == ZF_ACT_SWISH) {
+        const float sg = sigmoidf(z[t]);
+        x[t] = x[t] * (sg + z[t] * sg * (1.0f - sg));
+      } else {
+        x[t] = x[t] * act_other_grad(act, z[t]);
+      }
+    }
+  }
+  *reinterpret_cast<float4*>(C + o) = float4{x[0], x[1], x[2], x[3]};
+}
+
 // SPLITQ: block z = q of a 64 x 64 tile multiplies only the k-pairs
 // p = q (mod 4) — exactly accumulator set q of the NACC = 4 kernel, in the
 // same order (trailing all-zero pairs aside, which only turn -0 into +0) —
@@ -265,6 +299,196 @@ __global__ void gemm_small_k_kernel(int M, int N, int K, const float* __restrict
   gemm_epilogue(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
 }
 
+// ---- Large-batch GEMMs on bf16x3 split MFMA ----------------------------------
+// C = A . op(B) (A row-major [M][K]; B row-major [K][N], or [N][K] when TB)
+// with every fp32 operand split into three RNE bf16 terms (x = hi + mid + lo)
+// and six v_mfma_f32_32x32x16_bf16 products per k-step, small terms first —
+// an fp32 dot product to ~1e-7 relative (the inference kernels' bf16x3
+// scheme, zf_flow_x3_kernel.h), at 419 TFLOP/s fp32-equivalent peak against
+// the fp32 MFMA's 157.  Block tile 128 x 128 x 32, 4 waves in 2 x 2, each
+// 64 x 64 as 2 x 2 MFMA tiles.  The split is done once per element, when a
+// k-tile is stored to LDS: LDS holds three bf16 planes of A ([m][k]) and of
+// B ([n][k]), rows of 32 k padded to 80 B (the 16 rows of a ds_read_b128
+// lane group land on 16 distinct 4-bank slots), so the inner loop is
+// fragment reads and MFMAs only.  The next k-tile's global loads are in
+// flight in registers while the current one is multiplied; 60 KiB of LDS ->
+// 2 blocks per CU.  K % 8 == 0 (a ragged last k-tile is zero-filled).
+// Epilogue: when N and the output rows allow it (WIDE), B is the MFMA's
+// first operand, so a lane holds one output row's 4 consecutive columns per
+// register group (same products, same sums, same bits); the tile goes
+// through LDS and leaves as row-contiguous dwordx4 stores, whole 128-B lines.
+// The MFMA layout's 64 dword stores per lane were store-issue-bound: cfg5's
+// hidden layer 111 us with them, 70 us with dwordx4 row pieces
+// (tests/hip/gemm_probe.hip).  Same epilogues as mgemm_kernel.  Used when
+// the GLOBAL batch gives >= 512 such blocks; ZF_TRAIN_X3=0 keeps the fp32
+// kernel.
+typedef __bf16 tbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 tbf16x2 __attribute__((ext_vector_type(2)));
+typedef float tfloatx2 __attribute__((ext_vector_type(2)));
+constexpr int kX3BM = 128, kX3BN = 128, kX3BK = 32;
+constexpr int kX3RS = 40;                       // bf16 per LDS row (32 k + 8 pad = 80 B)
+constexpr int kX3Plane = 128 * kX3RS;           // bf16 per plane
+
+// three RNE bf16 terms of 8 fp32 values, stored to the three planes at p
+__device__ __forceinline__ void split3_store(const float (&x)[8], __bf16* p) {
+  tbf16x8 h, m, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const tfloatx2 v = {x[2 * i], x[2 * i + 1]};
+    const tbf16x2 vh = __builtin_convertvector(v, tbf16x2);
+    const tfloatx2 r = v - __builtin_convertvector(vh, tfloatx2);
+    const tbf16x2 vm = __builtin_convertvector(r, tbf16x2);
+    const tfloatx2 r2 = r - __builtin_convertvector(vm, tfloatx2);
+    const tbf16x2 vl = __builtin_convertvector(r2, tbf16x2);
+    h[2 * i] = vh[0]; h[2 * i + 1] = vh[1];
+    m[2 * i] = vm[0]; m[2 * i + 1] = vm[1];
+    l[2 * i] = vl[0]; l[2 * i + 1] = vl[1];
+  }
+  *reinterpret_cast<tbf16x8*>(p) = h;
+  *reinterpret_cast<tbf16x8*>(p + kX3Plane) = m;
+  *reinterpret_cast<tbf16x8*>(p + 2 * kX3Plane) = l;
+}
+
+template <bool TB, bool WIDE>
+__global__ __launch_bounds__(256) void gemm_x3_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                      int ldc, int epi, const float* __restrict__ bias,
+                                                      float* __restrict__ H, const float* __restrict__ Z, int act) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[6 * kX3Plane];
+  __bf16* const Ap = lds;
+  __bf16* const Bp = lds + 3 * kX3Plane;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 64;
+  const int m0 = blockIdx.y * kX3BM, n0 = blockIdx.x * kX3BN;
+  const int r = lane & 31, h = lane >> 5;
+  // row-major [rows][K] tiles (A; B when TB): thread -> row e >> 2 (e = tid,
+  // tid + 256), 8 consecutive k at 8 (e & 3) as two float4s
+  float4 ra[4], rb[4];
+  float rbs[16];
+  auto load_rows = [&](const float* P, int ld, int r0, int R, int k0, float4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, row = r0 + (e >> 2);
+      const float* src = P + (long long)row * ld + k0 + 8 * (e & 3);
+      const bool ok = row < R && k0 + 8 * (e & 3) < K;
+      v[2 * i] = ok ? *reinterpret_cast<const float4*>(src) : float4{0.f, 0.f, 0.f, 0.f};
+      v[2 * i + 1] = ok ? *reinterpret_cast<const float4*>(src + 4) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_rows = [&](__bf16* P, const float4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      const float x[8] = {v[2 * i].x, v[2 * i].y, v[2 * i].z, v[2 * i].w,
+                          v[2 * i + 1].x, v[2 * i + 1].y, v[2 * i + 1].z, v[2 * i + 1].w};
+      split3_store(x, P + (e >> 2) * kX3RS + 8 * (e & 3));
+    }
+  };
+  // B row-major [K][N] (!TB): thread -> column n0 + (tid & 127), k 16 (tid >> 7) .. +15
+  auto load_cols = [&](int k0) {
+    const int n = n0 + (tid & 127);
+    const int kb = k0 + 16 * (tid >> 7);
+    const float* src = B + (long long)kb * ldb + n;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) rbs[j] = n < N && kb + j < K ? src[(long long)j * ldb] : 0.f;
+  };
+  auto store_cols = [&]() {
+    __bf16* P = Bp + (tid & 127) * kX3RS + 16 * (tid >> 7);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const float x[8] = {rbs[8 * g], rbs[8 * g + 1], rbs[8 * g + 2], rbs[8 * g + 3],
+                          rbs[8 * g + 4], rbs[8 * g + 5], rbs[8 * g + 6], rbs[8 * g + 7]};
+      split3_store(x, P + 8 * g);
+    }
+  };
+  auto load = [&](int k0) {
+    load_rows(A, lda, m0, M, k0, ra);
+    if (TB) load_rows(B, ldb, n0, N, k0, rb);
+    else load_cols(k0);
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += kX3BK) {
+    store_rows(Ap, ra);
+    if (TB) store_rows(Bp, rb);
+    else store_cols();
+    __syncthreads();
+    if (k0 + kX3BK < K) load(k0 + kX3BK);
+#pragma unroll
+    for (int s = 0; s < kX3BK / 16; ++s) {
+      tbf16x8 af[2][3], bf[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          af[i][t] = *reinterpret_cast<const tbf16x8*>(Ap + t * kX3Plane + (wm0 + 32 * i + r) * kX3RS + 16 * s + 8 * h);
+          bf[i][t] = *reinterpret_cast<const tbf16x8*>(Bp + t * kX3Plane + (wn0 + 32 * i + r) * kX3RS + 16 * s + 8 * h);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          // WIDE: B as the MFMA's first operand, so D = C^T: lane = row m and
+          // each group of 4 registers = 4 consecutive columns (one dwordx4
+          // store; the same products and sums, the same bits)
+          auto mf = [&](int ta, int tb, const floatx16& c) {
+            return WIDE ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[j][tb], af[i][ta], c, 0, 0, 0)
+                        : __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][ta], bf[j][tb], c, 0, 0, 0);
+          };
+          floatx16 c = mf(1, 1, acc[i][j]);  // (A term, B term): m m, h l, l h, h m, m h, h h
+          c = mf(0, 2, c);
+          c = mf(2, 0, c);
+          c = mf(0, 1, c);
+          c = mf(1, 0, c);
+          acc[i][j] = mf(0, 0, c);
+        }
+    }
+    __syncthreads();
+  }
+  if (WIDE) {
+    // through LDS (free after the loop's last barrier), per wave and per
+    // 32-row half: ds_write_b128 of each lane's row pieces (row pitch 68
+    // floats: conflict-free), then row-contiguous float4s — each store
+    // instruction writes 4 rows x 256 B, whole 128-B lines
+    float* T = reinterpret_cast<float*>(lds) + wave * (32 * 68);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(T + r * 68 + 32 * j + 8 * g + 4 * h) =
+              float4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int row = 4 * t + (lane >> 4), c4 = lane & 15;
+        const float4 v = *reinterpret_cast<const float4*>(T + row * 68 + 4 * c4);
+        const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 4 * c4;
+        if (m < M && n < N) gemm_epilogue4(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
+        if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+      }
+}
+
 template <int T>
 void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
                  hipStream_t st, int epi, const float* bias, float* H, const float* Z, int act) {
@@ -292,6 +516,31 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
   if (M <= 0 || N <= 0) return ZF_OK;
   const long long big = (long long)((N + 127) / 128) * ((Mg + 127) / 128);
   const long long tiles64 = (long long)((N + 63) / 64) * ((M + 63) / 64);
+  static const bool x3_ok = [] {
+    const char* e = std::getenv("ZF_TRAIN_X3");
+    return !(e && e[0] == '0');
+  }();
+  const bool a_ok = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+  const bool b_ok = !tb || (ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  if (big >= 512 && x3_ok && K % 8 == 0 && a_ok && b_ok) {
+    const dim3 grid((N + kX3BN - 1) / kX3BN, (M + kX3BM - 1) / kX3BM);
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool wide = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!H || al16(H)) && (!Z || al16(Z)) &&
+                      (!bias || al16(bias));
+#define ZF_X3_LAUNCH(TB_, W_)                                                                                    \
+  hipLaunchKernelGGL((gemm_x3_kernel<TB_, W_>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, \
+                     H, Z, act)
+    if (tb) {
+      if (wide) ZF_X3_LAUNCH(true, true);
+      else ZF_X3_LAUNCH(true, false);
+    } else {
+      if (wide) ZF_X3_LAUNCH(false, true);
+      else ZF_X3_LAUNCH(false, false);
+    }
+#undef ZF_X3_LAUNCH
+    ZF_CHECK_LAUNCH("gemm_x3_kernel");
+    return ZF_OK;
+  }
   if (big >= 512) {
     gemm_launch<128>(tb, M, N, K, A, lda, B, ldb, C, ldc, st, epi, bias, H, Z, act);
   } else if (split != nullptr && !tb && K <= 8) {
