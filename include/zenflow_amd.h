@@ -133,7 +133,7 @@ typedef struct zf_op_desc {
   /* NSC */
   int32_t knots;      /* K (2 <= K <= 64) */
   int32_t n_hidden;   /* number of hidden Dense layers (len(layers)), 1..16 */
-  int32_t hidden[16]; /* widths of the hidden layers (each <= 256) */
+  int32_t hidden[16]; /* widths of the hidden layers (each <= 4096; > 256: the layered path) */
   int32_t act;        /* ZF_ACT_* */
   int32_t _pad;
   /* Offsets (in floats) into the NATURAL parameter blob, filled by
@@ -189,6 +189,7 @@ int zf_flow_destroy(zf_flow_t* handle);
 #define ZF_KERNEL_FP32 0
 #define ZF_KERNEL_BF16X3 1
 #define ZF_KERNEL_F16X2 2
+#define ZF_KERNEL_LAYERED 3 /* a hidden width > 256: op by op (BatchNorm, GEMMs, spline kernels) */
 int zf_flow_kernel_variant(const zf_flow_t* h);
 
 /* Device workspace needed by zf_flow_log_prob for N rows. */

@@ -56,7 +56,13 @@ CONFIGS = {
     # one activation per coupling (a Chain of differently configured couplings)
     "mixed": dict(D=4, C=0, K=16, layers=(128, 128), latent="normal", act=("relu", "swish", "gelu", "tanh")),
     "mixed_fp32": dict(D=3, C=0, K=8, layers=(64,), latent="normal", act=("swish", "sigmoid", "elu")),
+    # hidden widths above 256 (layer_utils.rect / tri build any width): the
+    # layered path (BatchNorm, the trainer's GEMMs, per-(row, dim) spline kernels)
+    "h512": dict(D=4, C=0, K=16, layers=(512, 512), latent="normal"),
+    "h384c2": dict(D=3, C=2, K=8, layers=(384,), latent="beta", act="gelu"),
+    "h1024k5": dict(D=5, C=0, K=5, layers=(1024, 64), latent="truncated_normal", couplings=2),
 }
+LAYERED = ["h512", "h384c2", "h1024k5"]
 ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu", "mixed", "mixed_fp32"]
 
 

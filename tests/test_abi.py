@@ -84,7 +84,7 @@ def test_flow_plan_offsets_cfg2():
     [
         (1, [(3, 16, (128,))], ValueError),  # NSC needs D >= 2
         (4, [(3, 0, (128,))], ValueError),  # knots < 1
-        (4, [(3, 16, (300,))], NotImplementedError),  # width > 256
+        (4, [(3, 16, (5000,))], NotImplementedError),  # width > 4096 (257..4096 run layered)
         (4, [(9,)], ValueError),  # unknown op
     ],
 )

@@ -74,11 +74,11 @@ def check_lp(lp, case, tag=""):
 
 WIDE_SHAPES = ["d6", "d8", "d16", "d7k32c2", "d4k32", "d3k32", "d4h256k8", "d5h64"]
 PADK_SHAPES = ["k12", "k5c1", "k15", "k24h256", "k3", "small", "odd", "uniform"]  # padded knots
-from tests.flowcases import ACTS  # noqa: E402  (NeuralSplineCoupling.act other than swish)
+from tests.flowcases import ACTS, LAYERED  # noqa: E402  (NeuralSplineCoupling.act other than swish; > 256 wide)
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg4c1", "small", "odd", "uniform", "deep", "d3c1", "d2h256"]
-                         + WIDE_SHAPES + ACTS + ["k12", "k5c1", "k15", "k24h256", "k3"])
+                         + WIDE_SHAPES + ACTS + ["k12", "k5c1", "k15", "k24h256", "k3"] + LAYERED)
 @pytest.mark.parametrize("N", [1, 1000, 4096])
 def test_log_prob_parity(name, N):
     case = make_case(name, N=N, seed=11)
@@ -91,7 +91,7 @@ def test_log_prob_parity_cfg5():
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "small", "odd", "deep", "cfg5", "d3c1", "d2h256"] + WIDE_SHAPES
-                         + ["relu", "gelu", "sigmoid", "softplus", "k12", "k5c1", "k24h256"])
+                         + ["relu", "gelu", "sigmoid", "softplus", "k12", "k5c1", "k24h256"] + LAYERED)
 def test_inverse_parity(name):
     case = make_case(name, N=2000, seed=13)
     rng = np.random.default_rng(7)
@@ -107,7 +107,7 @@ def test_inverse_parity(name):
     assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
 
 
-@pytest.mark.parametrize("name", ["cfg2", "odd", "cfg4", "d3c1", "d2h256", "d8", "d7k32c2", "d4h256k8"])
+@pytest.mark.parametrize("name", ["cfg2", "odd", "cfg4", "d3c1", "d2h256", "d8", "d7k32c2", "d4h256k8"] + LAYERED)
 def test_chain_forward_parity(name):
     """Chain.__call__ (y, log_det) vs the oracle's chain."""
     case = make_case(name, N=3000, seed=14)
@@ -551,3 +551,36 @@ def test_two_set_kernel_parity(name, monkeypatch):
     assert np.mean(fin != np.isfinite(x)) <= 1e-3
     both = fin & np.isfinite(x)
     assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
+
+
+@pytest.mark.parametrize("name", LAYERED)
+def test_layered_path(name):
+    """Hidden widths above 256 run op by op (zf_layered.hip): the handle
+    reports it, log_prob over several row chunks (a 1024-wide layer holds
+    65536 rows per chunk) matches the oracle on sampled rows, the NLL
+    partials reduce to the sum of the returned log_prob, and forward then
+    inverse returns x."""
+    from zenflow_amd import _lib as L
+
+    N = 70000 if name == "h1024k5" else 5000
+    case = make_case(name, N=N, seed=21)
+    cfg = case["cfg"]
+    flow = build_flow(cfg)
+    bf = flow.bind(case["variables"], cfg["D"], cfg["C"])
+    prog = bf.program
+    assert prog.kernel_variant == "layered"
+    x = L.DeviceArray.from_numpy(case["x"])
+    c = None if case["c"] is None else L.DeviceArray.from_numpy(case["c"])
+    nll = L.DeviceArray((1,), np.float64)
+    lp = prog.log_prob(x, c, nll_sum=nll).numpy()
+    fin = np.abs(lp) < 1e38
+    total = float(nll.numpy()[0])
+    assert abs(total - lp[fin].astype(np.float64).sum()) <= 1e-6 * max(1.0, np.abs(lp[fin]).sum())
+    rows = np.r_[0:200, N - 200:N, 65400:65700] if N > 65700 else np.r_[0:N]
+    sub = {k: v[rows] if isinstance(v, np.ndarray) else v for k, v in case.items()}
+    check_lp(lp[rows], sub, f"{name}/layered")
+    y, ld = prog.forward(x, c)
+    xr = prog.inverse(y, c).numpy()
+    ok = np.isfinite(xr).all(axis=1) & np.isfinite(ld.numpy())
+    assert ok.mean() > 0.99
+    assert_allclose(xr[ok], case["x"][ok], rtol=1e-4, atol=1e-4)

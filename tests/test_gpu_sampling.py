@@ -82,7 +82,7 @@ def test_latent_sample_errors():
     assert lib.zf_latent_sample(L.ZF_LATENT_NORMAL, 0.0, 1, z.ptr, 0, 2, None) == 0
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg1", "cfg4", "small", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg1", "cfg4", "small", "cfg5", "h512", "h384c2"])
 def test_flow_sample_equals_inverse_of_latent(name):
     """zf_flow_sample (latent drawn in the inverse kernel's prologue) ==
     Chain.inverse(Distribution.sample) bit for bit, on both fused kernels."""

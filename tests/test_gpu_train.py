@@ -125,7 +125,9 @@ GRAD_CASES = CASES + [("cfg1", 1024, 66), ("d8", 512, 67), ("d2h256", 256, 68), 
                       ("relu", 256, 70), ("gelu", 256, 71), ("tanh", 256, 72), ("softplus", 256, 73),
                       ("sigmoid", 256, 74), ("elu", 256, 75), ("leaky_relu", 256, 76), ("mixed", 256, 77),
                       # a batch whose forward Dense layers run the bf16x3 split-MFMA GEMM (>= 512 128x128 tiles)
-                      ("cfg2", 65536, 79), ("cfg5", 32768, 78)]
+                      ("cfg2", 65536, 79), ("cfg5", 32768, 78),
+                      # hidden 512 / 384 (the eval path for these widths is the layered one)
+                      ("h512", 256, 83), ("h384c2", 256, 84)]
 
 
 @pytest.mark.parametrize("name,N,seed", GRAD_CASES)

@@ -42,6 +42,7 @@ ZF_SB_UPPER = 3
 ZF_KERNEL_FP32 = 0
 ZF_KERNEL_BF16X3 = 1
 ZF_KERNEL_F16X2 = 2
+ZF_KERNEL_LAYERED = 3
 
 
 class ZfOpDesc(C.Structure):

@@ -350,6 +350,10 @@ int hidden_pad_of(const zf_flow_desc* desc) {
   return hp;
 }
 
+// Widths up to 256 run in the fused kernels; wider ones on the layered path
+// (zf_layered.hip), whose row chunks shrink as the width grows.
+constexpr int kMaxFusedWidth = 256, kMaxLayeredWidth = 4096;
+
 int validate(const zf_flow_desc* desc) {
   if (!desc) return einval("desc is NULL");
   if (desc->dim < 1 || desc->dim > 64) return einval("dim %d out of range [1, 64]", desc->dim);
@@ -363,7 +367,8 @@ int validate(const zf_flow_desc* desc) {
       if (op.knots < 1 || op.knots > 64) return einval("knots %d out of range [1, 64]", op.knots);
       if (op.n_hidden < 1 || op.n_hidden > 16) return enotsup("n_hidden must be in [1, 16]");
       for (int l = 0; l < op.n_hidden; ++l)
-        if (op.hidden[l] < 1 || op.hidden[l] > 256) return enotsup("hidden width must be in [1, 256]");
+        if (op.hidden[l] < 1 || op.hidden[l] > kMaxLayeredWidth)
+          return enotsup("hidden width must be in [1, 4096]");
       if (op.act < 0 || op.act >= ZF_ACT_COUNT) return einval("op %d: unknown activation %d", i, op.act);
     } else if (op.kind != ZF_OP_ROLL && op.kind != ZF_OP_SHIFT_BOUNDS) {
       return einval("op %d: unknown kind %d", i, op.kind);
@@ -388,6 +393,7 @@ struct zf_flow {
   int x4_pieces = 0;     // two-set kernel: KiB of small parameters in LDS (0: not used)
   int x4_ks0 = 0;
   int device = 0;
+  zf::LayeredFlow* lay = nullptr;  // layered eval path (a hidden width > 256), or null
 };
 
 namespace zf {
@@ -486,9 +492,12 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   F.latent = desc.latent;
   F.n_ops = desc.n_ops;
   F.HP = zf::hidden_pad_of(&desc);
+  // a conditioner wider than the fused kernels hold runs layer by layer
+  const bool layered = F.HP > zf::kMaxFusedWidth;
+  if (layered) F.HP = 32;  // the fused layouts below are then not built
   int x3K = 0;
   // the split-MFMA kernel runs hidden <= 128 padded to 128 (4 tiles)
-  const bool x3 = zf::x3_eligible(desc, F.HP < 128 ? 128 : F.HP, &x3K);
+  const bool x3 = !layered && zf::x3_eligible(desc, F.HP < 128 ? 128 : F.HP, &x3K);
   if (x3 && F.HP < 128) F.HP = 128;
   const int HP = F.HP, T = HP / 32;
   // Latent constants in fp32, as jax.scipy.stats computes them.
@@ -525,6 +534,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       d.KS0 = g.KS0; d.T_last = g.T_last; d.nslot_mask = g.nslot - 1; d.act = op.act;
       nslot = g.nslot > nslot ? g.nslot : nslot;
       d.bn = take(3 * 2 * g.KS0);
+      if (layered) continue;  // BatchNorm rows only: the layered path reads the natural weights
       d.w[0] = take((int64_t)T * g.KS0 * 64);
       for (int l = 0; l < op.n_hidden; ++l) d.b[l] = take((int64_t)T * 32);
       d.b[op.n_hidden] = take((int64_t)g.T_last * 32);
@@ -538,7 +548,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   for (int i = 0; i < desc.n_ops; ++i) {
     const zf_op_desc& op = desc.ops[i];
     zf::DevOp& d = F.ops[i];
-    if (op.kind != ZF_OP_NSC) continue;
+    if (op.kind != ZF_OP_NSC || layered) continue;
     const zf::OpGeom g = zf::nsc_geom(&desc, op);
     for (int l = 1; l < op.n_hidden; ++l) d.w[l] = take((int64_t)T * T * 1024);
     d.w[op.n_hidden] = take((int64_t)g.T_last * T * 1024);
@@ -557,6 +567,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
     } else if (op.kind == ZF_OP_NSC) {
       const zf::OpGeom g = zf::nsc_geom(&desc, op);
       zf::pack_nsc_bn(&desc, op, nat, P + d.bn);
+      if (layered) continue;
       // layer 0: A fragment of (o, ks): lane l -> W0[k = 2ks + (l>>5)][i = 32o + (l&31)]
       {
         const int in = g.DC, out = op.hidden[0];
@@ -640,6 +651,13 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   const bool use_x3 = F.x3_ok != 0;
   int rcd = ZF_OK;
   hipError_t e = hipGetDevice(&h->device);
+  if (e == hipSuccess && layered) {
+    rcd = zf::layered_create(desc, nat, need, &h->lay);
+    if (rcd) {
+      zf_flow_destroy(h);
+      return rcd;
+    }
+  }
   if (e == hipSuccess && use_x3) e = hipMalloc(&h->d_x3, x3s.size() * sizeof(uint16_t));
   if (e == hipSuccess && use_x3)
     e = hipMemcpy(h->d_x3, x3s.data(), x3s.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
@@ -663,12 +681,14 @@ int zf_flow_destroy(zf_flow_t* h) {
   if (h->d_desc) (void)hipFree(h->d_desc);
   if (h->d_blob) (void)hipFree(h->d_blob);
   if (h->d_x3) (void)hipFree(h->d_x3);
+  zf::layered_destroy(h->lay);
   delete h;
   return ZF_OK;
 }
 
 int zf_flow_kernel_variant(const zf_flow_t* h) {
   if (!h) return -1;
+  if (h->lay) return ZF_KERNEL_LAYERED;
   return h->host.x3_ok == 2 ? ZF_KERNEL_F16X2 : h->host.x3_ok ? ZF_KERNEL_BF16X3 : ZF_KERNEL_FP32;
 }
 
@@ -692,6 +712,9 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
   if (N == 0) return ZF_OK;
   if (!x && !gen) return einval("x is NULL");
   if (h->host.C > 0 && !c) return einval("flow is conditional (C=%d) but c is NULL", h->host.C);
+  if (h->lay)
+    return layered_run(h->lay, h->host, h->d_blob, INV, op_begin, op_end, x, c, y, ld_in, ld_out, lp, part, N,
+                       (hipStream_t)stream, seed, gen);
   if (h->host.x3_ok) {
     X3Launch a;
     a.desc = h->d_desc; a.blob = h->d_blob; a.x3 = h->d_x3;

@@ -157,8 +157,35 @@ __device__ __forceinline__ void load_state(float* xs, const float* __restrict__ 
   }
 }
 
-// ShiftBounds on the state (bijectors.py:181-208 forward, eval branch of
-// :261-273; :210-240 inverse).  `sb` is the packed [D][8] row block.
+// ShiftBounds of one value of logical dim i (bijectors.py:181-208 forward,
+// eval branch of :261-273; :210-240 inverse).  r = the packed row sb + 8 i:
+// [mode, a, b, xmin, xmax, mul, log mul, 0].
+__device__ __forceinline__ float sb_forward_elem(const float* __restrict__ r, float v, float& l) {
+  const int mode = (int)r[0];
+  const float a = r[1], b = r[2], xmin = r[3];
+  const float mul = r[5], logmul = r[6];
+  if (mode == ZF_SB_BOTH) {  // :187-192
+    l = logmul;
+    return (v - a) * mul;
+  }
+  float t = v;
+  if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);  // safe_log :430
+  if (mode == ZF_SB_UPPER) t = logf((b - v) + 1.17549435e-38f);
+  const float zr = (t - xmin) * mul;
+  l = (mode == ZF_SB_NONE) ? logmul : logmul - t;    // :197, :202
+  return (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);  // :272 clip
+}
+
+__device__ __forceinline__ float sb_inverse_elem(const float* __restrict__ r, float zv) {
+  const int mode = (int)r[0];
+  const float a = r[1], b = r[2];
+  const float xmin = r[3], xmax = r[4];
+  if (mode == ZF_SB_BOTH) return zv * b + (1.f - zv) * a;
+  const float t = zv * xmax + (1.f - zv) * xmin;
+  return (mode == ZF_SB_LOWER) ? expf(t) + a : (mode == ZF_SB_UPPER ? b - expf(t) : t);
+}
+
+// ShiftBounds on the per-wave state.  `sb` is the packed [D][8] row block.
 template <bool INV>
 __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, float* xs, int s, int hh,
                                                 int rot, int D, float& ld) {
@@ -166,22 +193,8 @@ __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, fl
     float ldsb = 0.f;
     for (int i = 0; i < D; ++i) {
       const int p = wrap(i + rot, D);
-      const float v = xs[p * 32 + s];
-      const int mode = (int)sb[8 * i];
-      const float a = sb[8 * i + 1], b = sb[8 * i + 2], xmin = sb[8 * i + 3];
-      const float mul = sb[8 * i + 5], logmul = sb[8 * i + 6];
-      float z, l;
-      if (mode == ZF_SB_BOTH) {  // :187-192
-        z = (v - a) * mul;
-        l = logmul;
-      } else {
-        float t = v;
-        if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);  // safe_log :430
-        if (mode == ZF_SB_UPPER) t = logf((b - v) + 1.17549435e-38f);
-        const float zr = (t - xmin) * mul;
-        z = (zr != zr) ? zr : fminf(fmaxf(zr, 0.f), 1.f);  // :272 clip
-        l = (mode == ZF_SB_NONE) ? logmul : logmul - t;    // :197, :202
-      }
+      float l;
+      const float z = sb_forward_elem(sb + 8 * i, xs[p * 32 + s], l);
       ldsb = ldsb + l;
       if (hh == 0) xs[p * 32 + s] = z;
     }
@@ -189,17 +202,7 @@ __device__ __forceinline__ void shift_bounds_op(const float* __restrict__ sb, fl
   } else {
     for (int i = 0; i < D; ++i) {
       const int p = wrap(i + rot, D);
-      const float zv = xs[p * 32 + s];
-      const int mode = (int)sb[8 * i];
-      const float a = sb[8 * i + 1], b = sb[8 * i + 2];
-      const float xmin = sb[8 * i + 3], xmax = sb[8 * i + 4];
-      float xv;
-      if (mode == ZF_SB_BOTH) {
-        xv = zv * b + (1.f - zv) * a;
-      } else {
-        const float t = zv * xmax + (1.f - zv) * xmin;
-        xv = (mode == ZF_SB_LOWER) ? expf(t) + a : (mode == ZF_SB_UPPER ? b - expf(t) : t);
-      }
+      const float xv = sb_inverse_elem(sb + 8 * i, xs[p * 32 + s]);
       if (hh == 0) xs[p * 32 + s] = xv;
     }
   }
@@ -253,6 +256,41 @@ __device__ __forceinline__ void layer0(const DevOp& op, const float* __restrict_
       for (int r = 0; r < 16; ++r) hb[o][r] = swish(hb[o][r]);
 }
 
+// One coordinate's latent log-density (distributions.py:16-126, the
+// jax.scipy.stats forms) with the DevFlow latent constants.
+__device__ __forceinline__ float latent_logpdf(int lt, float c0, float c1, float c2, float v) {
+  float t;
+  if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
+    // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
+    const float dv = v - 0.5f;
+    t = (c0 + (dv * dv) / c1) / -2.0f;
+    if (lt == ZF_LATENT_TRUNCNORM) {  // - log mass; -inf outside [-5, 5] sigma
+      t = t - c2;
+      const float xsd = dv / 0.1f;
+      if (xsd < -5.f || xsd > 5.f) t = -INFINITY;
+    }
+  } else if (lt == ZF_LATENT_BETA) {
+    // -betaln(a,a) + xlogy(a-1, x) + xlog1py(a-1, -x); -inf outside [0, 1]
+    const float l1 = (c1 == 0.f) ? 0.f : c1 * logf(v);
+    const float l2 = (c1 == 0.f) ? 0.f : c1 * log1pf(-v);
+    t = c0 + (l1 + l2);
+    if (v > 1.f || v < 0.f) t = -INFINITY;
+  } else {  // uniform
+    t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
+  }
+  return t;
+}
+
+// jnp.nan_to_num(lp, nan=-inf) (flow.py:47): JAX's sequential where chain,
+// each mask taken from the running result — NaN -> -inf -> finfo.min,
+// +inf -> finfo.max, -inf -> finfo.min.
+__device__ __forceinline__ float nan_to_num_lp(float lp) {
+  if (lp != lp) lp = -INFINITY;
+  if (lp == INFINITY) lp = 3.40282347e38f;
+  if (lp == -INFINITY) lp = -3.40282347e38f;
+  return lp;
+}
+
 // latent.log_prob(z) + log_det, nan_to_num (flow.py:41-48;
 // distributions.py:16-33), block partial of sum(log_prob) for the NLL, and
 // the optional y / log_det outputs.  Partials: block b writes part[b*pstride]
@@ -268,39 +306,10 @@ __device__ __forceinline__ void flow_epilogue(const DevFlow* __restrict__ F, con
                                               float* __restrict__ ld_out, double* s_part,
                                               long long slot = -1) {
   if (lp_out != nullptr) {
-    const int lt = F->latent;
-    const float c0 = F->lat_c0, c1 = F->lat_c1, c2 = F->lat_c2;
     float lat = 0.f;
-    for (int j = 0; j < D; ++j) {
-      const float v = xs[wrap(j + rot, D) * 32 + s];
-      float t;
-      if (lt == ZF_LATENT_NORMAL || lt == ZF_LATENT_TRUNCNORM) {
-        // jax.scipy.stats.norm.logpdf: (log(2 pi s^2) + (x-loc)^2/s^2) / -2
-        const float dv = v - 0.5f;
-        t = (c0 + (dv * dv) / c1) / -2.0f;
-        if (lt == ZF_LATENT_TRUNCNORM) {  // - log mass; -inf outside [-5, 5] sigma
-          t = t - c2;
-          const float xsd = dv / 0.1f;
-          if (xsd < -5.f || xsd > 5.f) t = -INFINITY;
-        }
-      } else if (lt == ZF_LATENT_BETA) {
-        // -betaln(a,a) + xlogy(a-1, x) + xlog1py(a-1, -x); -inf outside [0, 1]
-        const float l1 = (c1 == 0.f) ? 0.f : c1 * logf(v);
-        const float l2 = (c1 == 0.f) ? 0.f : c1 * log1pf(-v);
-        t = c0 + (l1 + l2);
-        if (v > 1.f || v < 0.f) t = -INFINITY;
-      } else {  // uniform
-        t = (v > 1.f || v < 0.f) ? -INFINITY : 0.f;
-      }
-      lat = lat + t;
-    }
-    float lp = lat + ld;
-    // jnp.nan_to_num(lp, nan=-inf) (flow.py:47): JAX's sequential where
-    // chain, each mask taken from the running result — NaN -> -inf ->
-    // finfo.min, +inf -> finfo.max, -inf -> finfo.min.
-    if (lp != lp) lp = -INFINITY;
-    if (lp == INFINITY) lp = 3.40282347e38f;
-    if (lp == -INFINITY) lp = -3.40282347e38f;
+    for (int j = 0; j < D; ++j)
+      lat = lat + latent_logpdf(F->latent, F->lat_c0, F->lat_c1, F->lat_c2, xs[wrap(j + rot, D) * 32 + s]);
+    const float lp = nan_to_num_lp(lat + ld);
     if (valid && hh == 0) lp_out[row] = lp;
     if (block_partial != nullptr) {
       double v = (valid && hh == 0) ? (double)lp : 0.0;
@@ -354,6 +363,15 @@ int launch_flow_x4(const X3Launch& a, bool inverse, int small_pieces, int ks0);
 bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0);
 size_t x4_lds_bytes_host(int K, bool one, int D, int C, int small_pieces);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
+// Layered eval path (zf_layered.hip) for shapes the fused kernels cannot hold
+// (a hidden width above 256): op by op over row chunks — BatchNorm, the Dense
+// layers on the trainer's GEMMs, the per-(row, dim) spline kernels.
+struct LayeredFlow;
+int layered_create(const zf_flow_desc& desc, const float* natural, int64_t n, LayeredFlow** out);
+void layered_destroy(LayeredFlow* L);
+int layered_run(LayeredFlow* L, const DevFlow& F, const float* packed, bool inverse, int op_begin, int op_end,
+                const float* x, const float* c, float* y, const float* ld_in, float* ld_out, float* lp, double* part,
+                long long N, hipStream_t st, unsigned long long seed, int gen);
 int x3_last_tiles(int K);
 int x3_pairs(const zf_flow_desc& desc);
 int x3_buf_tiles(const zf_flow_desc& desc, int T, int K);

@@ -44,4 +44,16 @@ inline int enotsup(const char* msg) {
 // Post-launch check: a bad launch configuration surfaces here.
 #define ZF_CHECK_LAUNCH(name) ZF_TRY_HIP(hipGetLastError())
 
+// Trainer pieces the layered eval path (zf_layered.hip) runs (zf_train.hip):
+// C = A . W + bias (W row-major [K][N], a FLAX Dense kernel) and, when H is
+// given, H = act(C) (the trainer's fused epilogue).  Mg: the batch that
+// picks the tile shape.
+int dense_gemm(long long Mg, int M, int N, int K, const float* A, int lda, const float* W, int ldw, float* C,
+               int ldc, float* H, hipStream_t st, const float* bias, int act);
+// One coupling's RQ spline over B rows from raw conditioner outputs P
+// [B][dt][3K-1] (normalize_spline_params + forward with log_det += into ld,
+// or inverse), state columns rotated by rot.
+int spline_rows(bool inverse, const float* s_in, float* s_out, const float* P, float* ld, int B, int D, int dt,
+                int K, int rot, hipStream_t st);
+
 }  // namespace zf

@@ -1287,6 +1287,61 @@ __global__ __launch_bounds__(kSplThreads) void spline_fwd_kernel(const float* __
   }
 }
 
+// Inverse (the layered eval path's Chain.inverse; utils.py:144-202): the same
+// per-(row, dim) layout and staging; knots normalized as spline_one forms
+// them, bin search and quadratic root as the fused kernels (zf_spline.h).
+struct RawKnots {
+  const float* p;
+  int K;
+  float Sa, Sb, rSa, rSb, cc, norm, rnorm;
+  __device__ float w(int j) const { return t_div(t_div(sp_f(p[j]), Sa, rSa) + cc, norm, rnorm); }
+  __device__ float h(int j) const { return t_div(t_div(sp_f(p[K + j]), Sb, rSb) + cc, norm, rnorm); }
+  __device__ float d(int j) const { return sp_f(p[2 * K + j]); }
+};
+
+__device__ __forceinline__ float spline_inv_one(const float* p, int K, float y) {
+  RawKnots q;
+  q.p = p;
+  q.K = K;
+  const double c64 = 1e-5 / (1.0 - (double)K * 1e-5);  // utils.py:32-34, Python floats
+  q.cc = (float)c64;
+  q.norm = (float)(1.0 + c64 * (double)K);
+  float Sa = 0.f, Sb = 0.f;
+  for (int j = 0; j < K; ++j) {
+    Sa = Sa + sp_f(p[j]);
+    Sb = Sb + sp_f(p[K + j]);
+  }
+  q.Sa = Sa;
+  q.Sb = Sb;
+  q.rSa = t_rcp(Sa);
+  q.rSb = t_rcp(Sb);
+  q.rnorm = t_rcp(q.norm);
+  const RqsBin b = rqs_bin<false>(y, K, q);
+  return rqs_inverse_eval(y, b);
+}
+
+__global__ __launch_bounds__(kSplThreads) void spline_inv_kernel(const float* __restrict__ s_in,
+                                                                 float* __restrict__ s_out,
+                                                                 const float* __restrict__ P, int B, int D, int dt,
+                                                                 int K, int rot) {
+  extern __shared__ float sp[];
+  const int S = 3 * K - 1, rpb = kSplThreads / dt;
+  const int lr = threadIdx.x / dt, d = threadIdx.x - lr * dt;
+  const long long b0 = (long long)blockIdx.x * rpb, b = b0 + lr;
+  const int nrows = (int)(B - b0 < rpb ? B - b0 : rpb);
+  const bool ok = lr < nrows;
+  const int col = pmodi(d + rot, D);
+  const float yv = ok ? s_in[b * D + col] : 0.f;
+  stage_rows(sp, P + b0 * dt * S, (long long)nrows * dt * S);
+  __syncthreads();
+  if (!ok) return;
+  for (int j = dt + d; j < D; j += dt) {
+    const int cj = pmodi(j + rot, D);
+    s_out[b * D + cj] = s_in[b * D + cj];
+  }
+  s_out[b * D + col] = spline_inv_one(sp + threadIdx.x * S, K, yv);
+}
+
 // Reverse: g_in = dL/d(state_in) from g_out = dL/d(state_out) and gl per row;
 // conditioning columns pass g_out through (their MLP share is added later).
 // dL/dP is formed in place in the staged rows and written back coalesced.
@@ -2116,3 +2171,34 @@ int zf_trainer_set_blob(zf_trainer_t* t, const float* blob_host) {
 }
 
 }  // extern "C"
+
+// ---- Entry points of the layered eval path (zf_layered.hip) -----------------
+namespace zf {
+
+int dense_gemm(long long Mg, int M, int N, int K, const float* A, int lda, const float* W, int ldw, float* C,
+               int ldc, float* H, hipStream_t st, const float* bias, int act) {
+  return gemm(false, Mg, M, N, K, A, lda, W, ldw, C, ldc, st, bias ? kEpiBias : kEpiNone, bias, H, nullptr, act);
+}
+
+int spline_rows(bool inverse, const float* s_in, float* s_out, const float* P, float* ld, int B, int D, int dt,
+                int K, int rot, hipStream_t st) {
+  if (B <= 0) return ZF_OK;
+  if (dt < 1 || dt > kSplThreads || K < 1 || K > kMaxK) return enotsup("spline rows: transformed dims or knots out of range");
+  const int S = 3 * K - 1, rpb = kSplThreads / dt;
+  const size_t lds = (size_t)kSplThreads * S * sizeof(float);
+  if (inverse) {
+    hipLaunchKernelGGL(spline_inv_kernel, dim3(blocks_for(B, rpb)), dim3(kSplThreads), lds, st, s_in, s_out, P, B,
+                       D, dt, K, rot);
+    ZF_CHECK_LAUNCH("spline_inv_kernel");
+    return ZF_OK;
+  }
+#define ZF_SPL(KTV)                                                                                          \
+  hipLaunchKernelGGL((spline_fwd_kernel<KTV>), dim3(blocks_for(B, rpb)), dim3(kSplThreads), lds, st, s_in, \
+                     s_out, P, ld, B, D, dt, K, rot)
+  ZF_KNOT_DISPATCH(K, ZF_SPL);
+#undef ZF_SPL
+  ZF_CHECK_LAUNCH("spline_fwd_kernel");
+  return ZF_OK;
+}
+
+}  // namespace zf

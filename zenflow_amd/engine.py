@@ -142,9 +142,10 @@ class Program:
 
     @property
     def kernel_variant(self) -> str:
-        """'f16x2', 'bf16x3' or 'fp32': the fused kernel this chain runs (zf_flow_kernel_variant)."""
+        """'f16x2', 'bf16x3' or 'fp32': the fused kernel this chain runs, or 'layered' (a hidden
+        width above 256: op by op on GEMMs and spline kernels; zf_flow_kernel_variant)."""
         v = L.load_library().zf_flow_kernel_variant(ct.c_void_p(self.handle))
-        return {L.ZF_KERNEL_F16X2: "f16x2", L.ZF_KERNEL_BF16X3: "bf16x3"}.get(v, "fp32")
+        return {L.ZF_KERNEL_F16X2: "f16x2", L.ZF_KERNEL_BF16X3: "bf16x3", L.ZF_KERNEL_LAYERED: "layered"}.get(v, "fp32")
 
     def __del__(self):
         h = getattr(self, "handle", None)
