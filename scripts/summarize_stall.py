@@ -24,9 +24,14 @@ def main(tag="r02", src=ROOT / "gpurun_out", prefix="pmc_st", label="cfg2"):
     (cfg2 also refreshes the bench's pmc_traffic.json entry)."""
     agg = {}
     kname = None
+    # the bench run also launches its configs block: keep the label's own
+    # instantiation only (template arguments as in scripts/trace_vs_bench.py)
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from trace_vs_bench import KERNELS
+    want = KNAME + KERNELS[label][0] if KNAME == "flow_kernel_x3" and label in KERNELS else KNAME
     for path in glob.glob(str(Path(src) / f"{prefix}*" / "run_counter_collection.csv")):
         for r in csv.DictReader(open(path)):
-            if KNAME not in r["Kernel_Name"]:
+            if want not in r["Kernel_Name"]:
                 continue
             if int(r.get("Grid_Size") or r["Grid_Size_X"]) < (1 << 20):
                 continue
