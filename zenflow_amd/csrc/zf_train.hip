@@ -113,12 +113,13 @@ __device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, flo
 // into part[q][M][N]; gemm_combine_kernel then forms
 // (P0 + P1) + (P2 + P3) and the epilogue: the same bits from four times the
 // blocks (small batches: 1024 rows give 32 tiles for 256 CUs).
-template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
-__global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
-                                                    const float* __restrict__ B, int ldb, float* __restrict__ C,
-                                                    int ldc, int epi, const float* __restrict__ bias,
-                                                    float* __restrict__ H, const float* __restrict__ Z, int KC,
-                                                    int act) {
+// The block body, with the block's coordinates passed in (mgemm_kernel: its
+// blockIdx; wgrad_group_kernel: decoded from one launch over several GEMMs).
+template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ>
+__device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K, const float* __restrict__ A, int lda,
+                                           const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
+                                           int epi, const float* __restrict__ bias, float* __restrict__ H,
+                                           const float* __restrict__ Z, int KC, int act) {
   constexpr int NA = BM * MBK / 256, NB = BN * MBK / 256;  // tile elements per thread
   constexpr int TM = BM / 64, TN = BN / 64;                // 32x32 tiles per wave
   __shared__ float As[MBK][BM + 1];
@@ -126,12 +127,12 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = WG ? blockIdx.z * KC : 0;
+  const int m0 = bid.y * BM, n0 = bid.x * BN;
+  const int kbeg = WG ? bid.z * KC : 0;
   // SPLITQ: block q runs a virtual k range holding only its k-pairs
   // p = q, q + 4, q + 8, ... (virtual pair v = real pair 4 v + q), so one
   // k-tile of loads serves 16 of its pairs instead of 4
-  const int q4 = SPLITQ ? (int)blockIdx.z : 0;
+  const int q4 = SPLITQ ? (int)bid.z : 0;
   const int kend = WG ? min(K, kbeg + KC) : SPLITQ ? 2 * max(0, ((K + 1) / 2 - q4 + 3) / 4) : K;
   auto real_k = [&](int k) { return SPLITQ ? 2 * (4 * (k >> 1) + q4) + (k & 1) : k; };
   const int kmax = SPLITQ ? K : kend;
@@ -178,11 +179,11 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[q][i][j] = floatx16{0};
-  // bias-gradient column sums (WG, blockIdx.y == 0): column cc, k-quarter cq
+  // bias-gradient column sums (WG, bid.y == 0): column cc, k-quarter cq
   constexpr int CQ = 256 / BN, CK = MBK / CQ;
   const int cc = tid % BN, cq = tid / BN;
   float csum = 0.f;
-  const bool do_cs = WG && blockIdx.y == 0;
+  const bool do_cs = WG && bid.y == 0;
   const int r = lane & 31, h = lane >> 5;
   if (kbeg < kend) load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += MBK) {
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
                                  : acc[0][i][j] + acc[1][i][j];
   }
   if (SPLITQ) {
-    float* P = C + (long long)blockIdx.z * M * N;
+    float* P = C + (long long)bid.z * M * N;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int m = m0 + wm0 + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + r;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
     return;
   }
   if (WG) {
-    float* P = C + (long long)blockIdx.z * (M + 1) * N;
+    float* P = C + (long long)bid.z * (M + 1) * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -258,6 +259,16 @@ __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const f
         const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
         if (m < M && n < N) gemm_epilogue(acc[0][i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
       }
+}
+
+
+template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
+__global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                    const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                    int ldc, int epi, const float* __restrict__ bias,
+                                                    float* __restrict__ H, const float* __restrict__ Z, int KC,
+                                                    int act) {
+  mgemm_body<BM, BN, TA, TB, WG, SPLITQ>(uint3{blockIdx.x, blockIdx.y, blockIdx.z}, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, H, Z, KC, act);
 }
 
 __global__ void gemm_combine_kernel(int M, int N, const float* __restrict__ P, float* __restrict__ C, int ldc,
@@ -781,13 +792,60 @@ __global__ __launch_bounds__(256) void wgrad_tree_batch(TreeBatch tb) {
   else t.db[idx - (long long)t.M * t.N] = v;
 }
 
+// Weight-gradient GEMMs deferred into one launch: each problem is the
+// mgemm_kernel<64, 64, TA, !TB, WG> grid it would have launched on its own
+// (the same blocks, the same bits), laid end to end.
+struct WgGemm {
+  const float *A, *G;
+  float* part;
+  int M, N, B, rows, tx, ty, block0;
+};
+constexpr int kWgGroup = 8;
+struct WgGroup {
+  int count;
+  WgGemm g[kWgGroup];
+};
+
+__global__ __launch_bounds__(256) void wgrad_group_kernel(WgGroup grp) {
+  int i = 0;
+  while (i + 1 < grp.count && (int)blockIdx.x >= grp.g[i + 1].block0) ++i;
+  const WgGemm& g = grp.g[i];
+  int r = (int)blockIdx.x - g.block0;
+  const unsigned bx = r % g.tx;
+  r /= g.tx;
+  const unsigned by = r % g.ty, bz = r / g.ty;
+  mgemm_body<64, 64, true, false, true, false>(uint3{bx, by, bz}, g.M, g.N, g.B, g.A, g.M, g.G, g.N, g.part, g.N,
+                                               kEpiNone, nullptr, nullptr, nullptr, g.rows, (int)ZF_ACT_SWISH);
+}
+
 struct WgradQueue {
   TreeBatch tb;
+  WgGroup gq;        // GEMMs not launched yet
+  int gblocks = 0;   // their blocks
   int64_t used = 0;  // workspace floats holding pending partials
   int nmax = 1;
 };
 
+int wgrad_launch_gemms(WgradQueue& q, hipStream_t st) {
+  if (q.gq.count == 0) return ZF_OK;
+  hipLaunchKernelGGL(wgrad_group_kernel, dim3(q.gblocks), dim3(256), 0, st, q.gq);
+  ZF_CHECK_LAUNCH("wgrad_group_kernel");
+  q.gq.count = 0;
+  q.gblocks = 0;
+  return ZF_OK;
+}
+
+// Launch the deferred GEMMs before `p` (a buffer one of them reads) is
+// overwritten.
+int wgrad_before_write(WgradQueue& q, const float* p, hipStream_t st) {
+  for (int i = 0; i < q.gq.count; ++i)
+    if (q.gq.g[i].A == p || q.gq.g[i].G == p) return wgrad_launch_gemms(q, st);
+  return ZF_OK;
+}
+
 int wgrad_flush(WgradQueue& q, hipStream_t st) {
+  int rc = wgrad_launch_gemms(q, st);
+  if (rc) return rc;
   if (q.tb.count == 0) return ZF_OK;
   int blocks = 0;
   for (int i = 0; i < q.tb.count; ++i) blocks += q.tb.it[i].blocks;
@@ -816,10 +874,19 @@ int wgrad_deferred(WgradQueue& q, int M, int N, int B, const Leaves& lv, const f
   if (q.used + need > kWsFloats || q.tb.count == kTreeItems)
     if ((rc = wgrad_flush(q, st))) return rc;
   float* part = ws + q.used;
-  hipLaunchKernelGGL((mgemm_kernel<64, 64, true, false, true>), dim3((N + 63) / 64, (M + 63) / 64, lv.n), dim3(256), 0,
-                     st, M, N, B, A, M, G, N, part, N, kEpiNone, nullptr, nullptr, nullptr, lv.rows,
-                     (int)ZF_ACT_SWISH);
-  ZF_CHECK_LAUNCH("mgemm_kernel<wgrad>");
+  if (q.gq.count == kWgGroup && (rc = wgrad_launch_gemms(q, st))) return rc;
+  WgGemm& g = q.gq.g[q.gq.count++];
+  g.A = A;
+  g.G = G;
+  g.part = part;
+  g.M = M;
+  g.N = N;
+  g.B = B;
+  g.rows = lv.rows;
+  g.tx = (N + 63) / 64;
+  g.ty = (M + 63) / 64;
+  g.block0 = q.gblocks;
+  q.gblocks += g.tx * g.ty * lv.n;
   TreeItem& it = q.tb.it[q.tb.count++];
   it.part = part;
   it.dW = dW;
@@ -913,43 +980,45 @@ inline int launch_tree_cols(const double* part, int n, long long N, double* out,
 // ---- ShiftBounds (train mode; bijectors.py:163-273) -------------------------
 // Natural row per dim: [mode, a, b, xmin, xmax, margin, -, -].  Batch min/max
 // of the (safe_log-transformed) column -> running xmin/xmax (:250-259).
-__global__ void sb_stats_kernel(float* __restrict__ sb, int D, const float* __restrict__ cmin,
-                                const float* __restrict__ cmax, int update) {
-  const int i = threadIdx.x;
-  if (i >= D) return;
-  float* r = sb + 8 * i;
-  if ((int)r[0] == ZF_SB_BOTH) return;
-  const float margin = r[5];
-  float lo = cmin[i], hi = cmax[i];
-  const float delta = 0.5f * (hi - lo) * margin;
-  lo = lo - delta;
-  hi = hi + delta;
-  lo = fminf(r[3], lo);  // jnp.minimum(ra_min, xmin); NaN from the batch propagates below
-  hi = fmaxf(r[4], hi);
-  if (cmin[i] != cmin[i]) lo = cmin[i];
-  if (cmax[i] != cmax[i]) hi = cmax[i];
-  if (update) { r[3] = lo; r[4] = hi; }
-  r[6] = lo;  // this step's values (used by sb_forward_kernel)
-  r[7] = hi;
-}
-
+// This batch's min / max widened by the margin and merged with the running
+// values, then the affine map, clip and log-det.  Every thread forms the
+// statistics from the column min / max itself (a handful of scalars: no
+// separate statistics launch); thread 0 also writes the running values when
+// update is set — the one write another block can observe, and re-forming
+// the statistics from it gives the same values (min / max are idempotent).
+// first: this op starts the chain, so ld (not yet written this step) is set
+// instead of accumulated.
 __global__ void sb_forward_kernel(const float* __restrict__ x, float* __restrict__ y, float* __restrict__ ld,
-                                  const float* __restrict__ sb, int B, int D, int rot) {
+                                  float* __restrict__ sb, int B, int D, int rot, const float* __restrict__ cmin,
+                                  const float* __restrict__ cmax, int update, int first) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   float lds = 0.f;
   for (int i = 0; i < D; ++i) {
     const int p = pmodi(i + rot, D);
     const float v = x[(long long)b * D + p];
-    const float* r = sb + 8 * i;
+    float* r = sb + 8 * i;
     const int mode = (int)r[0];
-    const float a = r[1], bb = r[2], xmin = r[6], xmax = r[7];
+    const float a = r[1], bb = r[2];
     float z, l;
     if (mode == ZF_SB_BOTH) {
       const float mul = (float)(1.0 / ((double)bb - (double)a));
       z = (v - a) * mul;
       l = logf(mul);
     } else {
+      const float margin = r[5];
+      float xmin = cmin[i], xmax = cmax[i];
+      const float delta = 0.5f * (xmax - xmin) * margin;
+      xmin = xmin - delta;
+      xmax = xmax + delta;
+      xmin = fminf(r[3], xmin);  // jnp.minimum(ra_min, xmin); NaN from the batch propagates below
+      xmax = fmaxf(r[4], xmax);
+      if (cmin[i] != cmin[i]) xmin = cmin[i];
+      if (cmax[i] != cmax[i]) xmax = cmax[i];
+      if (update && b == 0) {
+        r[3] = xmin;
+        r[4] = xmax;
+      }
       const float mul = 1.0f / (xmax - xmin);
       float t = v;
       if (mode == ZF_SB_LOWER) t = logf((v - a) + 1.17549435e-38f);
@@ -961,7 +1030,7 @@ __global__ void sb_forward_kernel(const float* __restrict__ x, float* __restrict
     lds = lds + l;
     y[(long long)b * D + p] = z;
   }
-  ld[b] = ld[b] + lds;
+  ld[b] = (first ? 0.f : ld[b]) + lds;
 }
 
 // ---- NeuralSplineCoupling pieces --------------------------------------------
@@ -1487,9 +1556,16 @@ __global__ void scatter_gu_kernel(const float* __restrict__ gU, float* __restric
 // lp = latent.log_prob(z) + log_det, nan_to_num (flow.py:45-47); per-row
 // loss terms -lp/Bg (fp64, summed by the leaf tree); gz = -(1/Bg) d latent_lp
 // / dz (zero where lp is not finite).  Bg: the global batch size.
-__global__ void latent_loss_kernel(const float* __restrict__ z, const float* __restrict__ ld, int B, long long Bg,
-                                   int D, int rot, int latent, float a, float betac, float tnmass,
-                                   float* __restrict__ gz, double* __restrict__ row_loss) {
+// leaf_rows > 0 (a divisor of the 256-row block): the block also forms the
+// loss leaf sums of its rows in row order, as leaf_sum_kernel does, into
+// leaf[block's leaves], the last block zeroing leaves past the last row
+// (one launch fewer per step).
+__global__ __launch_bounds__(256) void latent_loss_kernel(const float* __restrict__ z, const float* __restrict__ ld,
+                                                          int B, long long Bg, int D, int rot, int latent, float a,
+                                                          float betac, float tnmass, float* __restrict__ gz,
+                                                          double* __restrict__ row_loss, int leaf_rows,
+                                                          int leaf_n, double* __restrict__ leaf) {
+  __shared__ double rl[256];
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) {
     float lat = 0.f;
@@ -1529,7 +1605,22 @@ __global__ void latent_loss_kernel(const float* __restrict__ z, const float* __r
       }
       gz[(long long)b * D + col] = s * g;
     }
+    rl[threadIdx.x] = -(double)lp / (double)Bg;
   }
+  if (leaf_rows <= 0) return;
+  __syncthreads();
+  const int per = 256 / leaf_rows, z0 = blockIdx.x * 256;
+  if ((int)threadIdx.x < per) {
+    const int r0 = z0 + threadIdx.x * leaf_rows;
+    if (r0 < B) {
+      const int r1 = min(B, r0 + leaf_rows);
+      double acc = 0.0;
+      for (int r = r0; r < r1; ++r) acc += rl[r - z0];
+      leaf[r0 / leaf_rows] = acc;
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1)  // the leaves past the last row are empty (0, as leaf_sum_kernel)
+    for (int zl = (B + leaf_rows - 1) / leaf_rows + (int)threadIdx.x; zl < leaf_n; zl += 256) leaf[zl] = 0.0;
 }
 
 // ShiftBounds batch min / max of every rank (all-gathered [world][2][64]:
@@ -1548,9 +1639,15 @@ __global__ void minmax_ranks_kernel(const float* __restrict__ gath, int world, i
   cmax[i] = hi;
 }
 
-__global__ void cast_f64_f32_kernel(const double* __restrict__ x, long long n, float* __restrict__ y) {
+__device__ __forceinline__ void step_update(float* __restrict__ bc, float b1, float b2);
+
+// bc != NULL: thread 0 also advances the optimiser's step counter (the step
+// graph's launch before adam_kernel; step_kernel otherwise).
+__global__ void cast_f64_f32_kernel(const double* __restrict__ x, long long n, float* __restrict__ y,
+                                    float* __restrict__ bc = nullptr, float b1 = 0.f, float b2 = 0.f) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) y[i] = (float)x[i];
+  if (bc && i == 0) step_update(bc, b1, b2);
 }
 
 // ---- optimiser: optax adamw / nadamw ---------------------------------------
@@ -1559,7 +1656,7 @@ __global__ void cast_f64_f32_kernel(const double* __restrict__ x, long long n, f
 // Step count and bias corrections on the device (so a captured step graph
 // replays correctly): bc[0] = step t (as float bits of an int), bc[1] =
 // 1 - b1^t, bc[2] = 1 - b1^(t+1), bc[3] = 1 - b2^t.
-__global__ void step_kernel(float* __restrict__ bc, float b1, float b2) {
+__device__ __forceinline__ void step_update(float* __restrict__ bc, float b1, float b2) {
   int* cnt = reinterpret_cast<int*>(bc);
   const int t = *cnt + 1;
   *cnt = t;
@@ -1567,6 +1664,8 @@ __global__ void step_kernel(float* __restrict__ bc, float b1, float b2) {
   bc[2] = (float)(1.0 - pow((double)b1, (double)t + 1.0));
   bc[3] = (float)(1.0 - pow((double)b2, (double)t));
 }
+
+__global__ void step_kernel(float* __restrict__ bc, float b1, float b2) { step_update(bc, b1, b2); }
 
 __global__ void adam_kernel(float* __restrict__ prm, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, const unsigned char* __restrict__ mask, long long n, float lr,
@@ -1850,7 +1949,10 @@ int dp_combine(zf_trainer_t* t, double* roots, long long n, hipStream_t st) {
 // Train-mode forward + loss + reverse pass from the staged batch of B rows
 // (this rank's shard of a global batch of Bg rows); the loss lands in
 // loss_slot(t), the gradient in G (natural blob layout, fp32).
-int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* G, hipStream_t st) {
+// step_in_cast: an optimiser update follows; the one-device gradient cast
+// advances its step counter (trainer_update then skips step_kernel).
+int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* G, hipStream_t st,
+                 bool* step_in_cast = nullptr) {
   const int D = t->D, C = t->C, W = t->comm.world;
   const float* c = t->d_c;
   const zf_flow_desc& desc = t->desc;
@@ -1862,7 +1964,9 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
   for (int i = 0; i < desc.n_ops; ++i)
     sp[i + 1] = desc.ops[i].kind == ZF_OP_ROLL ? sp[i] : t->d_state + (int64_t)(i + 1) * t->bmax * D;
   auto state = [&](int i) { return sp[i]; };
-  ZF_TRY_HIP(hipMemsetAsync(t->d_ld, 0, (size_t)B * sizeof(float), st));
+  // a leading ShiftBounds sets ld itself (sb_forward_kernel, first)
+  if (desc.n_ops == 0 || desc.ops[0].kind != ZF_OP_SHIFT_BOUNDS)
+    ZF_TRY_HIP(hipMemsetAsync(t->d_ld, 0, (size_t)B * sizeof(float), st));
   const Leaves lbn = leaves_for(B, Bg, W, kBnLeafCap);
   // the single-block BatchNorm kernels have no exchange point (one device only)
   const bool small_ok = W == 1 && t->bn_small;
@@ -1890,11 +1994,9 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
                            t->d_small, t->d_small + 64);
         ZF_CHECK_LAUNCH("minmax_ranks_kernel");
       }
-      hipLaunchKernelGGL(zf::sb_stats_kernel, dim3(1), dim3(64), 0, st, sb, D, t->d_small, t->d_small + 64,
-                         update_stats);
-      ZF_CHECK_LAUNCH("sb_stats_kernel");
       hipLaunchKernelGGL(zf::sb_forward_kernel, dim3(zf::blocks_for(B)), dim3(256), 0, st, sin, sout, t->d_ld, sb, B,
-                         D, rot);
+                         D, rot, (const float*)t->d_small, (const float*)(t->d_small + 64), update_stats,
+                         i == 0 ? 1 : 0);
       ZF_CHECK_LAUNCH("sb_forward_kernel");
     } else if (op.kind == ZF_OP_NSC) {
       int dt, dc, DC, S;
@@ -1958,14 +2060,19 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
   const float tnm = (float)std::log1p(-2.0 * 0.5 * std::erfc(5.0 / std::sqrt(2.0)));
   float* g = t->d_g0;
   float* g_prev = t->d_g1;
-  hipLaunchKernelGGL(zf::latent_loss_kernel, dim3(zf::blocks_for(B)), dim3(256), 0, st, state(desc.n_ops), t->d_ld,
-                     B, Bg, D, rot, lt, a, betac, tnm, g, t->d_rowloss);
-  ZF_CHECK_LAUNCH("latent_loss_kernel");
   {
     const Leaves ll = leaves_for(B, Bg, W, kLeafCap);
-    hipLaunchKernelGGL(leaf_sum_kernel, dim3(blocks_for(ll.n, 64)), dim3(64), 0, st, t->d_rowloss, B, ll.rows, ll.n,
+    // leaves that tile the 256-row blocks are summed inside the loss kernel
+    const bool fused = ll.rows > 0 && ll.rows <= 256 && 256 % ll.rows == 0;
+    hipLaunchKernelGGL(zf::latent_loss_kernel, dim3(zf::blocks_for(B)), dim3(256), 0, st, state(desc.n_ops),
+                       t->d_ld, B, Bg, D, rot, lt, a, betac, tnm, g, t->d_rowloss, fused ? ll.rows : 0, ll.n,
                        t->d_leaf);
-    ZF_CHECK_LAUNCH("leaf_sum_kernel");
+    ZF_CHECK_LAUNCH("latent_loss_kernel");
+    if (!fused) {
+      hipLaunchKernelGGL(leaf_sum_kernel, dim3(blocks_for(ll.n, 64)), dim3(64), 0, st, t->d_rowloss, B, ll.rows,
+                         ll.n, t->d_leaf);
+      ZF_CHECK_LAUNCH("leaf_sum_kernel");
+    }
     if ((rc = launch_tree_cols(t->d_leaf, ll.n, 1, loss_slot(t), st, t->d_leaf2))) return rc;
     if ((rc = dp_combine(t, loss_slot(t), 1, st))) return rc;
   }
@@ -1974,6 +2081,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
   const float gl = -1.0f / (float)Bg;  // d loss / d log_det of every op and row
   zf::WgradQueue wq;
   wq.tb.count = 0;
+  wq.gq.count = 0;
   for (int i = desc.n_ops - 1; i >= 0; --i) {
     const zf_op_desc& op = desc.ops[i];
     if (op.kind == ZF_OP_ROLL || op.kind == ZF_OP_SHIFT_BOUNDS) continue;  // Roll: index map; SB: first op
@@ -2005,6 +2113,7 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
       if (rc) return rc;
       // g_in = gout . W_l^T
       float* gin = l == 0 ? nb.gU : gbufs[which];
+      if ((rc = zf::wgrad_before_write(wq, gin, st))) return rc;  // a deferred dW GEMM still reads it
       // (through swish of layer l-1 when l > 0)
       rc = zf::gemm(true, Bg, B, in_w, out_w, gout, out_w, nat + op.off_w[l], out_w, gin, in_w, st,
                     l > 0 ? zf::kEpiDSwish : zf::kEpiNone, nullptr, nullptr, l > 0 ? nb.Z[l - 1] : nullptr, op.act,
@@ -2057,16 +2166,19 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
     ZF_CHECK_LAUNCH("tree_cols_cast_kernel");
   } else {
     hipLaunchKernelGGL(cast_f64_f32_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, G64,
-                       (long long)t->nat_floats, G);
+                       (long long)t->nat_floats, G, step_in_cast ? t->d_bc : nullptr, t->opt.b1, t->opt.b2);
     ZF_CHECK_LAUNCH("cast_f64_f32_kernel");
+    if (step_in_cast) *step_in_cast = true;
   }
   return ZF_OK;
 }
 
-int trainer_update(zf_trainer_t* t, hipStream_t st) {
+int trainer_update(zf_trainer_t* t, hipStream_t st, bool step_done = false) {
   const zf_optim_desc& o = t->opt;
-  hipLaunchKernelGGL(step_kernel, dim3(1), dim3(1), 0, st, t->d_bc, o.b1, o.b2);
-  ZF_CHECK_LAUNCH("step_kernel");
+  if (!step_done) {
+    hipLaunchKernelGGL(step_kernel, dim3(1), dim3(1), 0, st, t->d_bc, o.b1, o.b2);
+    ZF_CHECK_LAUNCH("step_kernel");
+  }
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(t->nat_floats)), dim3(256), 0, st, t->d_nat, t->d_grad, t->d_m,
                      t->d_v, t->d_mask, (long long)t->nat_floats, o.learning_rate, o.b1, o.b2, o.eps, o.weight_decay,
                      o.nesterov, t->d_bc);
@@ -2088,8 +2200,9 @@ int step_graph(zf_trainer_t* t, int B, hipGraphExec_t* out) {
     t->graphs.clear();
   }
   ZF_TRY_HIP(hipStreamBeginCapture(t->cap, hipStreamCaptureModeThreadLocal));
-  int rc = trainer_body(t, B, B, 1, t->d_grad, t->cap);
-  if (!rc) rc = trainer_update(t, t->cap);
+  bool stepped = false;
+  int rc = trainer_body(t, B, B, 1, t->d_grad, t->cap, &stepped);
+  if (!rc) rc = trainer_update(t, t->cap, stepped);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(t->cap, &g);
   if (!rc && e != hipSuccess) rc = hip_status(e, "hipStreamEndCapture");
@@ -2142,8 +2255,9 @@ int zf_trainer_step_shard(zf_trainer_t* t, const float* x, const float* c, int64
     if (rc) return rc;
     ZF_TRY_HIP(hipGraphLaunch(exec, st));
   } else {
-    rc = zf::trainer_body(t, (int)rows, global_rows, 1, t->d_grad, st);
-    if (!rc) rc = zf::trainer_update(t, st);
+    bool stepped = false;
+    rc = zf::trainer_body(t, (int)rows, global_rows, 1, t->d_grad, st, &stepped);
+    if (!rc) rc = zf::trainer_update(t, st, stepped);
     if (rc) return rc;
   }
   t->t += 1;
