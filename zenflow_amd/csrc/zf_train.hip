@@ -1822,6 +1822,10 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   t->d_roots = (double*)zf::dmalloc(t, 2 * 256, rc);
   t->d_rowloss = (double*)zf::dmalloc(t, 2 * B, rc);
   t->d_g64 = (double*)zf::dmalloc(t, 2 * need, rc);
+  if (!rc) {
+    const hipError_t e = hipMemset(t->d_g64, 0, (size_t)need * sizeof(double));  // 2 need floats
+    if (e != hipSuccess) rc = zf::hip_status(e, "zf_trainer_create gradient");
+  }
   t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
   t->d_split = zf::dmalloc(t, zf::kSplitFloats, rc);
   t->d_c = zf::dmalloc(t, B * (desc.cond_dim > 0 ? desc.cond_dim : 1), rc);
@@ -2077,7 +2081,10 @@ int trainer_body(zf_trainer_t* t, int B, long long Bg, int update_stats, float* 
     if ((rc = dp_combine(t, loss_slot(t), 1, st))) return rc;
   }
   // ---- reverse ----
-  ZF_TRY_HIP(hipMemsetAsync(G64, 0, (size_t)t->nat_floats * sizeof(double), st));
+  // G64 needs no clearing per step: every parameter entry is assigned below
+  // (the weight-gradient trees, the BatchNorm scale / bias gradients) and the
+  // non-parameter entries (batch statistics, ShiftBounds rows) stay at the
+  // zeros written once at zf_trainer_create
   const float gl = -1.0f / (float)Bg;  // d loss / d log_det of every op and row
   zf::WgradQueue wq;
   wq.tb.count = 0;
