@@ -229,6 +229,9 @@ __global__ __launch_bounds__(256) void x3v(int M, int N, int K, const float* __r
       }
 }
 
+// the shipped kernel's persistent grid: min(tiles, 2 blocks per CU)
+inline dim3 x3grid(dim3 g) { return dim3(std::min(g.x * g.y, 512u)); }
+
 }  // namespace
 
 int main() {
@@ -269,7 +272,7 @@ int main() {
         const dim3 g3((N + 127) / 128, M / 128);
         const float tx3 = time_it(
             [&] {
-              hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), g3, dim3(256), 0, 0, M, N, K, A, K, B, N, C, N, epi,
+              hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), x3grid(g3), dim3(256), 0, 0, M, N, K, A, K, B, N, C, N, epi,
                                  bias, h, nullptr, ZF_ACT_SWISH);
             },
             20);
@@ -291,7 +294,7 @@ int main() {
       (void)hipMalloc(&C1, sizeof(float) * n);
       (void)hipMalloc(&C2, sizeof(float) * n);
       const dim3 g3((N + 127) / 128, M / 128);
-      hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), g3, dim3(256), 0, 0, M, N, K, A, K, B, N, C1, N,
+      hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), x3grid(g3), dim3(256), 0, 0, M, N, K, A, K, B, N, C1, N,
                          (int)zf::kEpiNone, bias, nullptr, nullptr, ZF_ACT_SWISH);
       hipLaunchKernelGGL((zf::mgemm_kernel<128, 128, false, false, false>), g3, dim3(256), 0, 0, M, N, K, A, K, B, N,
                          C2, N, (int)zf::kEpiNone, bias, nullptr, nullptr, 0, ZF_ACT_SWISH);
@@ -306,7 +309,7 @@ int main() {
       std::printf("N=%d  x3 vs fp32 MFMA: max |diff| / max |C| = %.3g\n", N, md / mx);
       hipLaunchKernelGGL((x3v<false, 1, 0, true>), g3, dim3(256), 0, 0, M, N, K, A, K, B, N, C2, N,
                          (int)zf::kEpiBias, bias, C, nullptr, ZF_ACT_SWISH);
-      hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), g3, dim3(256), 0, 0, M, N, K, A, K, B, N, C1, N,
+      hipLaunchKernelGGL((zf::gemm_x3_kernel<false, true>), x3grid(g3), dim3(256), 0, 0, M, N, K, A, K, B, N, C1, N,
                          (int)zf::kEpiBias, bias, H, nullptr, ZF_ACT_SWISH);
       {
         std::vector<float> w1(n), w2(n), q1(n), q2(n);
@@ -326,7 +329,7 @@ int main() {
       for (int k = 0; k < K; ++k)
         for (int j = 0; j < N; ++j) hbt[(size_t)j * K + k] = hb[(size_t)k * N + j];
       (void)hipMemcpy(Bt, hbt.data(), sizeof(float) * K * N, hipMemcpyHostToDevice);
-      hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), g3, dim3(256), 0, 0, M, N, K, A, K, Bt, K, C2, N,
+      hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), x3grid(g3), dim3(256), 0, 0, M, N, K, A, K, Bt, K, C2, N,
                          (int)zf::kEpiNone, bias, nullptr, nullptr, ZF_ACT_SWISH);
       (void)hipMemcpy(h2.data(), C2, sizeof(float) * n, hipMemcpyDeviceToHost);
       long long neq = 0;
@@ -334,7 +337,7 @@ int main() {
       std::printf("N=%d  x3 transposed-B form: %lld of %lld elements differ from the row-major form\n", N, neq, n);
       const float ttb = time_it(
           [&] {
-            hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), g3, dim3(256), 0, 0, M, N, K, A, K, Bt, K, C2, N,
+            hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), x3grid(g3), dim3(256), 0, 0, M, N, K, A, K, Bt, K, C2, N,
                                (int)zf::kEpiDSwish, bias, nullptr, C1, ZF_ACT_SWISH);
           },
           20);
@@ -367,7 +370,7 @@ int main() {
     const dim3 g3(N / 128, M / 128);
     const float tx = time_it(
         [&] {
-          hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), g3, dim3(256), 0, 0, M, N, K2, G, K2, W, K2, C, N,
+          hipLaunchKernelGGL((zf::gemm_x3_kernel<true, true>), x3grid(g3), dim3(256), 0, 0, M, N, K2, G, K2, W, K2, C, N,
                              (int)zf::kEpiDSwish, bias, nullptr, H, ZF_ACT_SWISH);
         },
         20);

@@ -361,7 +361,7 @@ __device__ __forceinline__ void split3_store(const float (&x)[8], __bf16* p) {
 }
 
 template <bool TB, bool WIDE>
-__global__ __launch_bounds__(256) void gemm_x3_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                       int ldc, int epi, const float* __restrict__ bias,
                                                       float* __restrict__ H, const float* __restrict__ Z, int act) {
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(int M, int N, int K, const
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 64;
-  const int m0 = blockIdx.y * kX3BM, n0 = blockIdx.x * kX3BN;
+  int m0 = 0, n0 = 0;  // the current output tile (the loop below)
   const int r = lane & 31, h = lane >> 5;
   // row-major [rows][K] tiles (A; B when TB): thread -> row e >> 2 (e = tid,
   // tid + 256), 8 consecutive k at 8 (e & 3) as two float4s
@@ -418,6 +418,14 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(int M, int N, int K, const
     if (TB) load_rows(B, ldb, n0, N, k0, rb);
     else load_cols(k0);
   };
+  // persistent blocks: a block takes output tiles blockIdx.x, + gridDim.x,
+  // ...; a tile's epilogue stores drain while the next tile's loads and
+  // MFMAs run (one launch round of blocks had every block storing at once)
+  const int tiles_n = (N + kX3BN - 1) / kX3BN;
+  const int ntiles = tiles_n * ((M + kX3BM - 1) / kX3BM);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  m0 = (tile / tiles_n) * kX3BM;
+  n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
   floatx16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -487,17 +495,19 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(int M, int N, int K, const
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
     }
-    return;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
+          if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+        }
   }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-        if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
-      }
+  __syncthreads();  // the next tile's planes overwrite the epilogue's LDS
+  }
 }
 
 template <int T>
@@ -534,7 +544,11 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
   const bool a_ok = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
   const bool b_ok = !tb || (ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0);
   if (big >= 512 && x3_ok && K % 8 == 0 && a_ok && b_ok) {
-    const dim3 grid((N + kX3BN - 1) / kX3BN, (M + kX3BM - 1) / kX3BM);
+    // two resident blocks per CU (60 KiB of LDS each), persistent over the tiles
+    const long long ntiles = (long long)((N + kX3BN - 1) / kX3BN) * ((M + kX3BM - 1) / kX3BM);
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const dim3 grid((unsigned)std::min<long long>(ntiles, 2ll * ncu));
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool wide = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!H || al16(H)) && (!Z || al16(Z)) &&
                       (!bias || al16(bias));
