@@ -175,17 +175,19 @@ int zf_flow_create(const zf_flow_desc* desc, const float* blob_host, int64_t blo
                    zf_flow_t** handle);
 int zf_flow_destroy(zf_flow_t* handle);
 
-/* Which fused kernel the handle runs (no reference counterpart: an
+/* Which kernel the handle runs (no reference counterpart: an
  * implementation detail made observable for tests and benchmarks):
- * ZF_KERNEL_FP32 (fp32 MFMA, any supported shape), or the split-MFMA kernel
- * for the shapes it covers (x3_eligible: every hidden width <= 256, one knot
- * count in {8, 16, 32} for all couplings, dim <= 64) in one of two
+ * ZF_KERNEL_FP32 (fp32 MFMA, any shape up to hidden 256), the split-MFMA
+ * kernel for the shapes it covers (x3_eligible: every hidden width <= 256,
+ * one knot count in 2..32 for all couplings — 8, 16, 32 instantiated, the
+ * others padded with inert knots, 31 excepted — dim <= 64) in one of two
  * schemes: ZF_KERNEL_F16X2 (default: two-term fp16 split of
  * power-of-two-scaled operands, three fp16 MFMAs per k-step) or
  * ZF_KERNEL_BF16X3 (three-term bf16 split, six bf16 MFMAs per k-step;
- * ZF_X3_SCHEME=bf16x3, where a softplus coupling runs on the fp32 kernel).  The
- * environment is read at zf_flow_create time; ZF_DISABLE_X3=1 forces
- * ZF_KERNEL_FP32.  -1 if h is NULL. */
+ * ZF_X3_SCHEME=bf16x3, where a softplus coupling runs on the fp32 kernel), or
+ * ZF_KERNEL_LAYERED (a hidden width above 256: op by op).  The environment
+ * is read at zf_flow_create time; ZF_DISABLE_X3=1 forces ZF_KERNEL_FP32 for
+ * fused shapes.  -1 if h is NULL. */
 #define ZF_KERNEL_FP32 0
 #define ZF_KERNEL_BF16X3 1
 #define ZF_KERNEL_F16X2 2
