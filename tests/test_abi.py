@@ -113,3 +113,17 @@ def test_no_gpu_fails_loudly(monkeypatch):
     with pytest.raises(RuntimeError):
         u.rational_quadratic_spline_forward(np.zeros((1, 1)), np.ones((1, 1, 1)), np.ones((1, 1, 1)),
                                             np.ones((1, 1, 0)))
+
+
+def test_header_constants_match_python():
+    """Every `#define ZF_<NAME> <int>` of include/zenflow_amd.h that the
+    Python side mirrors (`zenflow_amd._lib`) has the same value there."""
+    from zenflow_amd import _lib as L
+
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "zenflow_amd.h").read_text()
+    defs = dict(re.findall(r"^#define (ZF_[A-Z0-9_]+)\s+(-?\d+)\b", hdr, re.M))
+    assert "ZF_KERNEL_LAYERED" in defs
+    mirrored = [n for n in defs if hasattr(L, n)]
+    assert len(mirrored) >= 20, mirrored
+    for n in mirrored:
+        assert getattr(L, n) == int(defs[n]), n
