@@ -147,12 +147,13 @@ def test_rolling_spline_coupling():
     assert_allclose(x2, x, atol=1e-4)
 
 
-def test_train_mode_matches_oracle():
+@pytest.mark.parametrize("name", ["cfg4", "h384c2"])  # h384c2: a hidden width on the layered path
+def test_train_mode_matches_oracle(name):
     """Train-mode forward (batch statistics for ShiftBounds + BatchNorm) vs the
     oracle, and the running-average updates."""
     from tests.flowcases import build_flow, make_case
 
-    case = make_case("cfg4", N=3000, seed=31)
+    case = make_case(name, N=3000, seed=31)
     flow = build_flow(case["cfg"])
     lp, upd = flow.apply(case["variables"], case["x"], case["c"], train=True, mutable=["batch_stats"])
     ref, ref_stats = O.flow_log_prob(case["model"], case["variables"], case["x"], case["c"], train=True)
@@ -160,9 +161,11 @@ def test_train_mode_matches_oracle():
     assert np.mean(np.isfinite(ref) != np.isfinite(lp)) <= 1e-3
     assert_allclose(lp[fin], ref[fin], rtol=2e-5, atol=2e-5)
     got = upd["batch_stats"]["bijector"]
-    for k in ("xmin_0", "xmax_0", "xmin_1", "xmax_1"):
-        assert_allclose(got["bijectors_0"][k], ref_stats["bijectors_0"][k], rtol=1e-6)
-    for b in ("bijectors_1", "bijectors_3"):
+    D = case["cfg"]["D"]
+    for j in range(D):
+        for k in (f"xmin_{j}", f"xmax_{j}"):
+            assert_allclose(got["bijectors_0"][k], ref_stats["bijectors_0"][k], rtol=1e-6)
+    for b in [k for k in ref_stats if k != "bijectors_0" and "BatchNorm_0" in ref_stats[k]]:
         for k in ("mean", "var"):
             assert_allclose(got[b]["BatchNorm_0"][k], ref_stats[b]["BatchNorm_0"][k], rtol=1e-5, atol=1e-6)
 
