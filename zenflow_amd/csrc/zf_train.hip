@@ -543,6 +543,16 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
   }();
   const bool a_ok = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
   const bool b_ok = !tb || (ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0);
+  if (big >= 512 && !tb && K <= 8) {
+    // the first Dense (K = dc + C <= 8) at large batches too: one thread per
+    // output is bound by its Z / H stores, the MFMA tiles would multiply a
+    // 32-deep k-tile of zeros (the choice follows the global batch, as below)
+    const long long MN = (long long)M * N;
+    hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
+                       ldb, C, ldc, epi, bias, H, Z, act);
+    ZF_CHECK_LAUNCH("gemm_small_k_kernel");
+    return ZF_OK;
+  }
   if (big >= 512 && x3_ok && K % 8 == 0 && a_ok && b_ok) {
     // two resident blocks per CU (60 KiB of LDS each), persistent over the tiles
     const long long ntiles = (long long)((N + kX3BN - 1) / kX3BN) * ((M + kX3BM - 1) / kX3BM);
