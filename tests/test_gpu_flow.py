@@ -530,29 +530,6 @@ def test_trained_weights_parity(name, scheme, monkeypatch):
     _assert_strict(_strict_record(f"trained_{name}", lp, case, scheme))
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg4", "cfg1", "d3c1", "k12", "cfg4c1"])
-def test_two_set_kernel_parity(name, monkeypatch):
-    """The opt-in two-set kernel (ZF_X4=1, flow_kernel_x4: one wave per SIMD,
-    two 32-sample sets, one set's spline / layer 0 in the other's MFMA
-    slots; measured slower than flow_kernel_x3): log_prob,
-    inverse and ragged batches against the oracle, and Flow.sample equal to
-    the inverse of the latent draw."""
-    monkeypatch.setenv("ZF_X4", "1")
-    for N in (4096, 257, 1):
-        case = make_case(name, N=N, seed=41)
-        check_lp(gpu_log_prob(case), case, f"x4/{name}/N={N}")
-    case = make_case(name, N=2000, seed=42)
-    rng = np.random.default_rng(8)
-    z = (0.5 + 0.1 * rng.standard_normal(case["x"].shape)).astype(F32)
-    sub = {k: v["bijector"] for k, v in case["variables"].items()}
-    x = build_flow(case["cfg"]).bijector.apply(sub, z, case["c"], method="inverse")
-    ref = O.flow_inverse(case["model"], case["variables"], z, case["c"])
-    fin = np.isfinite(ref)
-    assert np.mean(fin != np.isfinite(x)) <= 1e-3
-    both = fin & np.isfinite(x)
-    assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
-
-
 @pytest.mark.parametrize("name", LAYERED)
 def test_layered_path(name):
     """Hidden widths above 256 run op by op (zf_layered.hip): the handle

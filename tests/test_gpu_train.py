@@ -261,12 +261,15 @@ def test_step_graph_matches_eager(monkeypatch):
         np.testing.assert_array_equal(flat[0][k], flat[1][k], err_msg=k)
 
 
-@pytest.mark.parametrize("name,N,seed", [("cfg2", 1024, 66), ("d2h256", 2048, 67), ("gelu", 512, 68), ("cfg4", 300, 69)])
+@pytest.mark.parametrize("name,N,seed", [("cfg2", 1024, 66), ("d2h256", 2048, 67), ("gelu", 512, 68), ("cfg4", 300, 69),
+                                         ("cfg1", 65536, 70)])
 def test_split_set_gemm_matches_single_kernel(name, N, seed, monkeypatch):
     """Small batches run the 64x64 GEMM tiles as four blocks, one per
     accumulator set of the interleaved kernel, plus a combine (SPLITQ in
     zf_train.hip): the same loss, gradient and trained parameters, bit for
-    bit, as the single-kernel form (ZF_TRAIN_SPLITQ=0)."""
+    bit, as the single-kernel form (ZF_TRAIN_SPLITQ=0).  At 65536 rows the
+    first Dense runs one thread per output under either setting (ADVICE r4:
+    the switch names the small-batch forms only)."""
     from zenflow_amd import _lib as L
 
     out = []

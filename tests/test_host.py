@@ -341,6 +341,45 @@ def test_setup_params_rebind_per_apply():
         m.b
 
 
+def test_setup_reads_declared_param():
+    """setup() may read a variable it has just declared (the flax
+    pattern ``self.w = self.param(...); self.n = self.w.shape[0]``) — on a
+    child and on the top-level module; outside init/apply it raises a clear
+    error instead of handing back a declaration object."""
+
+    class Child(zf.Module):
+        def setup(self):
+            self.w = self.param("w", lambda rng, shape: np.arange(shape[0], dtype=np.float32), (3,))
+            self.n = self.w.shape[0]
+            self.w2 = self.w * 2
+
+        def __call__(self, x):
+            return np.asarray(x, np.float32)[:, : self.n] * self.w2
+
+    class Top(zf.Module):
+        def setup(self):
+            self.child = Child()
+            self.b = self.param("b", lambda rng, shape: np.ones(shape, np.float32), (3,))
+            self.bs = float(self.b.sum())
+
+        def __call__(self, x):
+            return self.child(x) + self.bs
+
+    m = Top()
+    x = np.ones((2, 3), np.float32)
+    v = m.init(PRNGKey(0), x)
+    np.testing.assert_allclose(m.apply(v, x), x * np.arange(3) * 2 + 3.0)
+    assert m.child.n == 3  # derived in setup() from the declared param
+
+    class Lone(zf.Module):
+        def setup(self):
+            self.w = self.param("w", lambda rng: np.zeros(2, np.float32))
+            self.n = self.w.shape[0]
+
+    with pytest.raises(RuntimeError, match="outside init/apply"):
+        Lone().n
+
+
 def test_select_device_rules():
     """One rank per GPU: LOCAL_RANK picks the device; a rank masked down to
     one visible device uses it; ZF_DEVICE overrides (with a warning in a
@@ -349,7 +388,12 @@ def test_select_device_rules():
 
     assert select_device({}, 1) == 0
     assert select_device({"LOCAL_RANK": "3"}, 8) == 3
-    assert select_device({"LOCAL_RANK": "3", "WORLD_SIZE": "8"}, 1) == 0  # HIP_VISIBLE_DEVICES per rank
+    # masked down to one device per rank (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES per rank)
+    assert select_device({"LOCAL_RANK": "3", "WORLD_SIZE": "8", "HIP_VISIBLE_DEVICES": "3"}, 1) == 0
+    assert select_device({"LOCAL_RANK": "1", "WORLD_SIZE": "2", "ROCR_VISIBLE_DEVICES": "1"}, 1) == 0
+    # no mask — two ranks on a one-GPU node are oversubscribed and fail early
+    with pytest.raises(RuntimeError):
+        select_device({"LOCAL_RANK": "1", "WORLD_SIZE": "2"}, 1)
     with pytest.raises(RuntimeError):
         select_device({"LOCAL_RANK": "3"}, 2)
     assert select_device({"ZF_DEVICE": "1"}, 2) == 1

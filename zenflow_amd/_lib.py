@@ -216,9 +216,10 @@ def select_device(env, n: int) -> int:
     """The device index this process binds (one rank per GPU).
 
     * ``LOCAL_RANK`` (torchrun / our launcher) picks device LOCAL_RANK; when
-      the scheduler masks each rank down to ONE visible device
-      (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES per rank), LOCAL_RANK >= 1
-      maps to that device 0;
+      the scheduler masks each rank down to ONE visible device (a
+      HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES mask
+      is set), LOCAL_RANK >= 1 maps to that device 0 — without a mask, two
+      ranks on a one-GPU node are an oversubscribed launch and raise below;
     * ``ZF_DEVICE`` (explicit) overrides it — for ranks that share one GPU on
       purpose (HostAllgather tests); with WORLD_SIZE > 1 that puts several
       ranks on one device, so it warns;
@@ -235,8 +236,9 @@ def select_device(env, n: int) -> int:
                           f"{env.get('WORLD_SIZE')}-rank job (ranks sharing one GPU)", RuntimeWarning, stacklevel=3)
     else:
         dev = int(local or "0")
-        if n == 1 and dev >= 1:
-            dev = 0  # one visible device per rank
+        masked = any(env.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
+        if n == 1 and dev >= 1 and masked:
+            dev = 0  # the scheduler masked this rank down to its one device
     if not 0 <= dev < n:
         raise RuntimeError(
             f"zenflow_amd: device {dev} (LOCAL_RANK/ZF_DEVICE) is not visible; "

@@ -390,8 +390,7 @@ struct zf_flow {
   void* d_x3 = nullptr;       // bf16x3 weight-group stream (x3 kernel), or null
   int x3_K = 0;
   bool x3_oact = false;  // some coupling's activation is not swish
-  int x4_pieces = 0;     // two-set kernel: KiB of small parameters in LDS (0: not used)
-  int x4_ks0 = 0;
+  int x3_aset = 0;       // X3Launch::aset: which non-swish activations the flow uses
   int device = 0;
   zf::LayeredFlow* lay = nullptr;  // layered eval path (a hidden width > 256), or null
 };
@@ -639,13 +638,14 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
       if (desc.ops[i].kind == ZF_OP_NSC) F.kreal = desc.ops[i].knots;
     for (int i = 0; i < desc.n_ops; ++i)
       if (desc.ops[i].kind == ZF_OP_NSC && desc.ops[i].act != ZF_ACT_SWISH) h->x3_oact = true;
-    int ks0 = 0;
-    if (zf::x4_eligible(desc, HP, x3K, NT, h->x3_oact, &ks0)) {
-      const int pieces = (int)((F.small_floats * 4 + 1023) / 1024);
-      if (zf::x4_lds_bytes_host(x3K, desc.dim / 2 == 1, desc.dim, desc.cond_dim, pieces) <= 160 * 1024) {
-        h->x4_pieces = pieces;
-        h->x4_ks0 = ks0;
+    {
+      bool centred = false, plain = false;
+      for (int i = 0; i < desc.n_ops; ++i) {
+        if (desc.ops[i].kind != ZF_OP_NSC || desc.ops[i].act == ZF_ACT_SWISH) continue;
+        if (desc.ops[i].act == ZF_ACT_SIGMOID || desc.ops[i].act == ZF_ACT_SOFTPLUS) centred = true;
+        else plain = true;
       }
+      h->x3_aset = centred && plain ? 0 : centred ? 2 : 1;
     }
   }
   const bool use_x3 = F.x3_ok != 0;
@@ -723,11 +723,11 @@ int launch_flow(zf_flow* h, int op_begin, int op_end, const float* x, const floa
     a.op_begin = op_begin; a.op_end = op_end; a.N = N; a.K = h->x3_K; a.D = h->host.D; a.C = h->host.C; a.T = h->host.HP / 32;
     a.NT = h->host.x3_ok == 2 ? 2 : 3;
     a.oact = h->x3_oact;
+    a.aset = h->x3_aset;
     a.par_bytes = h->host.x3_par_bytes;
     a.seed = seed;
     a.gen = gen;
     a.stream = (hipStream_t)stream;
-    if (h->x4_pieces > 0) return launch_flow_x4(a, INV, h->x4_pieces, h->x4_ks0);
     return launch_flow_x3(a, INV);
   }
   const int64_t grid = (N + kBlockRows - 1) / kBlockRows;

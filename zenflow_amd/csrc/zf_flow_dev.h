@@ -37,6 +37,10 @@ struct DevOp {
   int x3_groups, x3_tlast;
   int x3_next[2];
   int x3_kw[17];  // f16x2: power-of-two weight scale of streamed layer l (1..n_hidden)
+  // f16x2 swish: per Dense_l (0..n_hidden-1, as packed: log2(e) prescale
+  // included) R = max_j sum_k |W[k][j]| and B = max_j |b[j]|, so every
+  // pre-activation |v_j| <= R * max_k |a_k| + B (x3_early_scale)
+  float x3_rb[16][2];
   // split-MFMA kernel: this NSC's small parameters (BatchNorm, Dense_0,
   // biases, the permuted last bias) are the contiguous blob floats
   // [bn, bn + 256 * x3_par_pieces), DMA'd into LDS one NSC ahead
@@ -353,15 +357,11 @@ struct X3Launch {
   int K, D, C, T;  // knots, dim, conditions, hidden tiles (4: width <= 128, 8: <= 256)
   int NT;       // split scheme: 3 = bf16x3, 2 = f16x2
   bool oact;    // some coupling's activation is not swish (f16x2 kernels with act switch)
+  int aset;     // oact, f16x2: 1 = only relu/tanh/gelu/elu/leaky_relu, 2 = only sigmoid/softplus, 0 = both kinds
   int par_bytes;  // DevFlow::x3_par_bytes
   hipStream_t stream;
 };
 int launch_flow_x3(const X3Launch& a, bool inverse);
-// Two-set kernel (zf_flow_x4_kernel.h): small_pieces = KiB of small
-// parameters staged in LDS, ks0 = Dense_0 k-steps
-int launch_flow_x4(const X3Launch& a, bool inverse, int small_pieces, int ks0);
-bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0);
-size_t x4_lds_bytes_host(int K, bool one, int D, int C, int small_pieces);
 bool x3_eligible(const zf_flow_desc& desc, int HP, int* K);
 // Layered eval path (zf_layered.hip) for shapes the fused kernels cannot hold
 // (a hidden width above 256): op by op over row chunks — BatchNorm, the Dense

@@ -100,33 +100,6 @@ int x3_param_of(int jp, int Kp, int K, float* fill) {
   return q < K - 1 ? 2 * K + q : -1;
 }
 
-// The two-set kernel (flow_kernel_x4): f16x2, every coupling swish with two
-// hidden layers (width <= 128), at most 2 transformed dims, <= 4 conditioner
-// inputs, one knot count in {8, 16, 32}, only Rolls between couplings.
-// Opt-in (ZF_X4=1): measured slower than flow_kernel_x3.
-bool x4_eligible(const zf_flow_desc& desc, int HP, int K, int NT, bool oact, int* ks0) {
-  const char* env = std::getenv("ZF_X4");
-  if (!(env && env[0] == '1')) return false;
-  if (NT != 2 || oact || HP != 128 || desc.dim / 2 > 2 || desc.dim < 2) return false;
-  // instantiated knot counts (K = 32 with two transformed dims spills)
-  if (!(K == 8 || K == 16 || (K == 32 && desc.dim / 2 == 1))) return false;
-  const int DC = desc.dim - desc.dim / 2 + desc.cond_dim;
-  if (DC > 4) return false;
-  int first = -1, last = -1;
-  for (int i = 0; i < desc.n_ops; ++i) {
-    const zf_op_desc& op = desc.ops[i];
-    if (op.kind != ZF_OP_NSC) continue;
-    if (op.n_hidden != 2 || op.act != ZF_ACT_SWISH) return false;
-    if (first < 0) first = i;
-    last = i;
-  }
-  if (first < 0) return false;
-  for (int i = first; i <= last; ++i)
-    if (desc.ops[i].kind != ZF_OP_NSC && desc.ops[i].kind != ZF_OP_ROLL) return false;
-  *ks0 = (DC + 1) / 2;
-  return true;
-}
-
 // Split scheme for new handles: ZF_X3_SCHEME=bf16x3 | f16x2 (default f16x2).
 int x3_scheme() {
   const char* env = std::getenv("ZF_X3_SCHEME");
@@ -275,6 +248,28 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
       for (int64_t i = 0; i < (int64_t)T * KS0 * 64; ++i) packed[d.w[0] + i] *= kSwishPrescale;
       for (int l = 0; l < op.n_hidden; ++l)
         for (int64_t i = 0; i < (int64_t)T * 32; ++i) packed[d.b[l] + i] *= kSwishPrescale;
+    }
+    // f16x2 swish: the per-layer pre-activation bounds of x3_early_scale
+    // (the prescaled weights and biases as the kernel multiplies them; fp64
+    // row sums rounded up by a relative 2^-20, so the float bound holds)
+    for (int l = 0; l < 16; ++l) d.x3_rb[l][0] = d.x3_rb[l][1] = 0.f;
+    if (NT == 2 && op.act == ZF_ACT_SWISH) {
+      const double pre = kSwishPrescale;
+      for (int l = 0; l < op.n_hidden && l < 16; ++l) {
+        const int in = l == 0 ? desc.dim - dt + desc.cond_dim : op.hidden[l - 1];
+        const int out = op.hidden[l];
+        const float* W = nat + op.off_w[l];
+        const float* Bv = nat + op.off_b[l];
+        double R = 0.0, Bm = 0.0;
+        for (int j = 0; j < out; ++j) {
+          double rs = 0.0;
+          for (int k = 0; k < in; ++k) rs += std::fabs((double)W[(int64_t)k * out + j]);
+          R = std::fmax(R, rs * pre);
+          Bm = std::fmax(Bm, std::fabs((double)Bv[j]) * pre);
+        }
+        d.x3_rb[l][0] = (float)(R * (1.0 + 0x1p-20));
+        d.x3_rb[l][1] = (float)(Bm * (1.0 + 0x1p-20));
+      }
     }
     // group-0 pieces of this NSC (hidden group, or a last-layer group when it has no hidden streamed layer)
     d.x3_npieces[0] = d.x3_npieces[1] = (2 * (op.n_hidden > 1 ? T : TL) * NT * 1024) >> 10;  // own; fixed below

@@ -6,7 +6,15 @@
 
 namespace zf {
 
+int launch_x3_k8_act1(const X3Launch& a, bool inverse);
+int launch_x3_k8_act2(const X3Launch& a, bool inverse);
+
+// f16x2 flows whose activations are all of one kind get the narrower
+// instantiations (zf_flow_x3_k8_act1 / _act2: the other kind's code out of
+// the register budget); mixed flows and bf16x3 take the full switch here.
 int launch_x3_k8_act(const X3Launch& a, bool inverse) {
+  if (a.NT == 2 && a.aset == 1) return launch_x3_k8_act1(a, inverse);
+  if (a.NT == 2 && a.aset == 2) return launch_x3_k8_act2(a, inverse);
   return a.NT == 2 ? launch_x3_k<2, 8, true>(a, inverse) : launch_x3_k<3, 8, true>(a, inverse);
 }
 

@@ -294,7 +294,11 @@ __device__ __forceinline__ void act_tile_plain<ZF_ACT_SIGMOID>(floatx16& t) {
   }
 }
 
-template <int NT, bool OACT>
+// ASET (f16x2 OACT kernels): the activations one instantiation takes besides
+// swish — 0: all of them (a flow mixing centred and plain activations),
+// 1: relu / tanh / gelu / elu / leaky_relu, 2: sigmoid / softplus (centred).
+// Narrower sets keep the other forms' code out of the register budget.
+template <int NT, bool OACT, int ASET = 0>
 __device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
   if constexpr (!OACT) {
 #pragma unroll
@@ -314,17 +318,31 @@ __device__ __forceinline__ void x3_act_tile(floatx16& t, float c, int act) {
         for (int r = 0; r < 16; ++r) t[r] = swish(t[r]);
     }
   } else {
-    switch (act) {
-      case ZF_ACT_RELU: act_tile_fixed<ZF_ACT_RELU>(t, c); break;
-      case ZF_ACT_TANH: act_tile_fixed<ZF_ACT_TANH>(t, c); break;
-      case ZF_ACT_GELU: act_tile_fixed<ZF_ACT_GELU>(t, c); break;
-      case ZF_ACT_ELU: act_tile_fixed<ZF_ACT_ELU>(t, c); break;
-      case ZF_ACT_LEAKY_RELU: act_tile_fixed<ZF_ACT_LEAKY_RELU>(t, c); break;
-      case ZF_ACT_SIGMOID: act_tile_centered<ZF_ACT_SIGMOID>(t, c); break;
-      case ZF_ACT_SOFTPLUS: act_tile_centered<ZF_ACT_SOFTPLUS>(t, c); break;
-      default:
+    if constexpr (ASET == 2) {
+      switch (act) {
+        case ZF_ACT_SIGMOID: act_tile_centered<ZF_ACT_SIGMOID>(t, c); break;
+        case ZF_ACT_SOFTPLUS: act_tile_centered<ZF_ACT_SOFTPLUS>(t, c); break;
+        default:
 #pragma unroll
-        for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+          for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+      }
+    } else {
+      switch (act) {
+        case ZF_ACT_RELU: act_tile_fixed<ZF_ACT_RELU>(t, c); break;
+        case ZF_ACT_TANH: act_tile_fixed<ZF_ACT_TANH>(t, c); break;
+        case ZF_ACT_GELU: act_tile_fixed<ZF_ACT_GELU>(t, c); break;
+        case ZF_ACT_ELU: act_tile_fixed<ZF_ACT_ELU>(t, c); break;
+        case ZF_ACT_LEAKY_RELU: act_tile_fixed<ZF_ACT_LEAKY_RELU>(t, c); break;
+        case ZF_ACT_SIGMOID:
+          if constexpr (ASET == 0) act_tile_centered<ZF_ACT_SIGMOID>(t, c);
+          break;
+        case ZF_ACT_SOFTPLUS:
+          if constexpr (ASET == 0) act_tile_centered<ZF_ACT_SOFTPLUS>(t, c);
+          break;
+        default:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) t[r] = act_swish<NT>(t[r], c);
+      }
     }
   }
 }
@@ -809,6 +827,13 @@ __device__ __forceinline__ void x3_slot(const char* lb, floatx16 (&hb)[T], float
   if constexpr (ks == 0) acc[o] = mfma_term2(fr[t & 1], cs, j, acc[o]);
   else acc[o] = mfma_term2(fr[t & 1], s1, j, acc[o]);
   x3_valu_slot<T, NOUT, Q, m>(hb, cs, s1, tq, s1h, csh, c);
+#if ZF_X3_ABL == 12 || ZF_X3_ABL == 13  // tuning: extra VALU in the group slots (12: v_add, 13: v_exp), 8 per group
+  if constexpr (j == 0) {
+    float dd;
+    if (ZF_X3_ABL == 12) asm volatile("v_add_f32 %0, %1, %2" : "=v"(dd) : "v"(acc[o][0]), "v"(acc[o][1]));
+    else asm volatile("v_exp_f32 %0, %1" : "=v"(dd) : "v"(acc[o][0]));
+  }
+#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -880,6 +905,253 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
   p.g += 1;
 }
 
+// Early per-sample scale (x3_early_scale, f16x2 swish at hidden 128): the
+// scale of a layer input from a bound instead of the exact maximum of the
+// previous layer's pre-activations, so it is known before that layer ends
+// and the layer's last group step can finish its tiles and swish + split the
+// next layer's tile 0 beside its own MFMAs (x3_step_slots_last) instead of
+// after them.  With R, B of DevOp::x3_rb, every pre-activation of Dense_l
+// obeys |v'_j| <= R_l * max_k |a_k| + B_l, and |swish(v)| <= |v| <= |v'|:
+// U_0 = R_0 max|u| + B_0 (u the BatchNorm'd conditioner inputs), U_l =
+// R_l U_{l-1} + B_l.  The scale is that of x3_act_scale with U in place of
+// the maximum (U >= the maximum, so no split operand exceeds 2^14); the split
+// terms of in-range values are the exact ones scaled by a power of two, so the
+// MFMA sums are the same bits as with the exact scale unless the bound is so
+// loose (> 2^13) that some residual terms fall below fp16's normal range.
+__device__ __forceinline__ void x3_scale_from(float U, int kw, float& isc, float& us, float& ius) {
+  const int e = max(__builtin_amdgcn_frexp_expf(U), -60);
+  isc = __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
+  us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
+  ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
+}
+
+// The last group step of a layer (Q = T-1) in tile-major order: slot m
+// multiplies (tile m / 6, k-step (m / 3) % 2, term m % 3), so tile o's sums
+// are complete after slot 6o+5; its finish (acc * us + bias, the bias read
+// two slots ahead) runs at slots 6o+7 / 6o+8, and NEXT: the next layer's
+// tile 0 is swished with its scale constant cn (exp at slot 9+i, fma 10+i,
+// rcp 11+i, mul 12+i for value i) and its k-step-0 split formed at slots
+// 20 / 21 (into cs, after the last k-step-0 MFMA of this step read it at
+// slot 20).  Stages past the last MFMA run after it in slot order.
+template <bool CR>
+__device__ __forceinline__ float x3_squareplus2_t(float x);
+
+template <int T, int NOUT, bool NEXT, int SPT, int m>
+__device__ __forceinline__ void x3_valu_slot_last(floatx16 (&hb)[T], floatx16 (&acc)[NOUT], halfx8 (&cs)[2],
+                                                  halfx8 (&s1)[2], float (&tq)[4], uint32_t (&s1h)[4],
+                                                  uint32_t (&csh)[4], floatx16& bt, const float* __restrict__ bias,
+                                                  int hh, float us, float cn, float& mx) {
+  constexpr int Q = T - 1;
+  if constexpr (m == 0) split8h_hi<1>(hb[Q], s1h);
+  if constexpr (m == 1) split8h_lo<1>(hb[Q], s1h, s1[0], s1[1]);
+  constexpr int ob = (m - 4) / 6;  // bias of tile ob read at slot 6 ob + 4
+  if constexpr (m >= 4 && (m - 4) % 6 == 0 && ob < NOUT) bt = bias_acc(bias + ob * 32, hh);
+  constexpr int of = (m - 7) / 6;  // finish of tile of at slots 6 of + 7 (values 0-7) and 6 of + 8 (8-15)
+  if constexpr (m >= 7 && of < NOUT && ((m - 7) % 6 == 0 || (m - 7) % 6 == 1)) {
+    constexpr int r0 = (m - 7) % 6 == 0 ? 0 : 8;
+#pragma unroll
+    for (int r = r0; r < r0 + 8; ++r) acc[of][r] = __builtin_fmaf(acc[of][r], us, bt[r]);
+  }
+  // SPT (the last layer): tiles 0..SPT-1 hold spline width / height logits,
+  // which the spline takes through 2 squareplus (x3_squareplus2): formed
+  // here, two values per slot from slot 6o+9, beside the remaining MFMAs
+#pragma unroll
+  for (int o2 = 0; o2 < SPT && o2 < NOUT; ++o2) {
+    const int rr = m - 9 - 6 * o2;  // compile-time after unrolling
+    if (rr >= 0 && rr < 8) {
+      acc[o2][2 * rr] = x3_squareplus2_t<false>(acc[o2][2 * rr]);
+      acc[o2][2 * rr + 1] = x3_squareplus2_t<false>(acc[o2][2 * rr + 1]);
+    }
+  }
+  // NEXT: the exact maximum |v'| of the finished values, one slot after their finish
+  constexpr int oq = (m - 8) / 6;
+  if constexpr (NEXT && m >= 8 && oq < NOUT && ((m - 8) % 6 == 0 || (m - 8) % 6 == 1)) {
+    constexpr int r0 = (m - 8) % 6 == 0 ? 0 : 8;
+#pragma unroll
+    for (int r = r0; r < r0 + 8; r += 2) mx = fmaxf(mx, fmaxf(fabsf(acc[oq][r]), fabsf(acc[oq][r + 1])));
+  }
+  if constexpr (NEXT) {
+    constexpr int i0 = m - 9, i1 = m - 10, i2 = m - 11, i3 = m - 12;
+    if constexpr (i3 >= 0 && i3 < 16) {
+      acc[0][i3] = acc[0][i3] * tq[i3 & 3];
+      asm volatile("" ::"v"(acc[0][i3]));
+    }
+    if constexpr (i2 >= 0 && i2 < 16) tq[i2 & 3] = __builtin_amdgcn_rcpf(tq[i2 & 3]);
+    if constexpr (i1 >= 0 && i1 < 16) tq[i1 & 3] = __builtin_fmaf(tq[i1 & 3], cn, cn);
+    if constexpr (i0 >= 0 && i0 < 16) tq[i0 & 3] = __builtin_amdgcn_exp2f(-acc[0][i0]);
+    if constexpr (m == 20) split8h_hi<0>(acc[0], csh);
+    if constexpr (m == 21) split8h_lo<0>(acc[0], csh, cs[0], cs[1]);
+  }
+}
+
+template <int T, int NOUT, bool NEXT, int SPT, int m>
+__device__ __forceinline__ void x3_slot_last(const char* lb, floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
+                                             halfx8 (&fr)[2][2], halfx8 (&cs)[2], halfx8 (&s1)[2], float (&tq)[4],
+                                             uint32_t (&s1h)[4], uint32_t (&csh)[4], floatx16& bt,
+                                             const float* __restrict__ bias, int hh, float us, float cn, float& mx) {
+  constexpr int t = m / 3, j = m % 3, o = t / 2, ks = t % 2;
+  constexpr int tn = t + 1, on = tn / 2, ksn = tn % 2;
+  if constexpr (j == 0 && tn < 2 * NOUT) load_frag<2>(lb + (((ksn * NOUT + on) * 2) << 10), fr[tn & 1]);
+  if constexpr (ks == 0) acc[o] = mfma_term2(fr[t & 1], cs, j, acc[o]);
+  else acc[o] = mfma_term2(fr[t & 1], s1, j, acc[o]);
+  x3_valu_slot_last<T, NOUT, NEXT, SPT, m>(hb, acc, cs, s1, tq, s1h, csh, bt, bias, hh, us, cn, mx);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int T, int NOUT, bool NEXT, int SPT, int... M>
+__device__ __forceinline__ void x3_slots_all_last(std::integer_sequence<int, M...>, const char* lb,
+                                                  floatx16 (&hb)[T], floatx16 (&acc)[NOUT], halfx8 (&fr)[2][2],
+                                                  halfx8 (&cs)[2], halfx8 (&s1)[2], float (&tq)[4],
+                                                  uint32_t (&s1h)[4], uint32_t (&csh)[4], floatx16& bt,
+                                                  const float* __restrict__ bias, int hh, float us, float cn,
+                                                  float& mx) {
+  (x3_slot_last<T, NOUT, NEXT, SPT, M>(lb, hb, acc, fr, cs, s1, tq, s1h, csh, bt, bias, hh, us, cn, mx), ...);
+}
+
+template <int T, int NOUT, bool NEXT, int SPT, int... M>
+__device__ __forceinline__ void x3_valu_tail_last(std::integer_sequence<int, M...>, floatx16 (&hb)[T],
+                                                  floatx16 (&acc)[NOUT], halfx8 (&cs)[2], halfx8 (&s1)[2],
+                                                  float (&tq)[4], uint32_t (&s1h)[4], uint32_t (&csh)[4],
+                                                  floatx16& bt, const float* __restrict__ bias, int hh, float us,
+                                                  float cn, float& mx) {
+  (x3_valu_slot_last<T, NOUT, NEXT, SPT, 6 * NOUT + M>(hb, acc, cs, s1, tq, s1h, csh, bt, bias, hh, us, cn, mx),
+   ...);
+}
+
+// A layer's last group step (see x3_valu_slot_last).  On return acc holds the
+// finished pre-activations acc * us + bias, and NEXT: tile 0 swished with the
+// next layer's constant cn and cs its k-step-0 split (what the next layer's
+// first x3_step_slots expects of hb[0] / cs).
+template <int T, int NOUT, bool NEXT, int SPT = 0>
+__device__ __forceinline__ void x3_step_slots_last(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                                   floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                                   int hh, halfx8 (&cs)[2], float us, float cn, float& mx) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<2, T>(x3, p, p.nxt, lane);
+  const char* lb = p.cur + lane * 16;
+  halfx8 fr[2][2];
+  load_frag<2>(lb, fr[0]);
+  halfx8 s1[2];
+  float tq[4];
+  uint32_t s1h[4], csh[4];
+  floatx16 bt;
+  constexpr int kSlots = 6 * NOUT;
+  constexpr int kEnd0 = NEXT ? (6 * NOUT > 28 ? 6 * NOUT : 28) : 6 * (NOUT - 1) + 9;
+  constexpr int kEnd = SPT > 0 && 6 * (SPT - 1) + 17 > kEnd0 ? 6 * (SPT - 1) + 17 : kEnd0;
+  mx = 0.f;
+  x3_slots_all_last<T, NOUT, NEXT, SPT>(std::make_integer_sequence<int, kSlots>{}, lb, hb, acc, fr, cs, s1, tq, s1h,
+                                        csh, bt, bias, hh, us, cn, mx);
+  x3_valu_tail_last<T, NOUT, NEXT, SPT>(std::make_integer_sequence<int, (kEnd > kSlots ? kEnd - kSlots : 0)>{}, hb,
+                                        acc, cs, s1, tq, s1h, csh, bt, bias, hh, us, cn, mx);
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+
+// Fused swish + split (ZF_X3_FUSED): the hi / lo fp16 terms of the exact
+// product v' * r of act_swish (one rounding each, v_fma_mix{lo,hi}: hi =
+// RN16(v' r), lo = RN16(v' r - hi)) instead of the fp32 product, a
+// conversion and the residual: 2 VALU per value instead of 2.5.  Value 2p of
+// a k-step goes to the low halves of h[p] / l[p], value 2p + 1 to the high
+// halves.  Their consumers are MFMAs of the next group step (behind its
+// barrier), so no hazard pad is needed here.
+template <int ODD>
+__device__ __forceinline__ void mix_hi(uint32_t& h, float v, float r) {
+  if constexpr (ODD == 0) asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(v), "v"(r));
+  else asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(v), "v"(r));
+}
+template <int ODD>
+__device__ __forceinline__ void mix_lo(uint32_t& l, float v, float r, uint32_t h) {
+  if constexpr (ODD == 0)
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(v), "v"(r), "v"(h));
+  else
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(v), "v"(r), "v"(h));
+}
+
+// Slot m's VALU in the fused schedule: Q == 0 splits its k-step 1 at slots
+// 0 / 1 (tile 0 arrives swished in fp32); tile Q+1 runs as a 5-stage modulo
+// pipeline, value i: exp at slot i+1, fma at i+2, rcp at i+3, hi at i+4, lo
+// at i+5, into nh / nl (pairs 0-3: k-step 0, 4-7: k-step 1).
+template <int T, int NOUT, int Q, int m>
+__device__ __forceinline__ void x3_valu_slot_f(floatx16 (&hb)[T], halfx8 (&s1)[2], uint32_t (&s1h)[4],
+                                               float (&tq)[5], uint32_t (&nh)[8], uint32_t (&nl)[8], float c) {
+  if constexpr (Q == 0 && m == 0) split8h_hi<1>(hb[0], s1h);
+  if constexpr (Q == 0 && m == 1) split8h_lo<1>(hb[0], s1h, s1[0], s1[1]);
+  if constexpr (Q + 1 < T) {
+    constexpr int i0 = m - 1, i1 = m - 2, i2 = m - 3, i3 = m - 4, i4 = m - 5;
+    if constexpr (i4 >= 0 && i4 < 16) mix_lo<i4 & 1>(nl[i4 >> 1], hb[Q + 1][i4], tq[i4 % 5], nh[i4 >> 1]);
+    if constexpr (i3 >= 0 && i3 < 16) mix_hi<i3 & 1>(nh[i3 >> 1], hb[Q + 1][i3], tq[i3 % 5]);
+    if constexpr (i2 >= 0 && i2 < 16) tq[i2 % 5] = __builtin_amdgcn_rcpf(tq[i2 % 5]);
+    if constexpr (i1 >= 0 && i1 < 16) tq[i1 % 5] = __builtin_fmaf(tq[i1 % 5], c, c);
+    if constexpr (i0 >= 0 && i0 < 16) tq[i0 % 5] = __builtin_amdgcn_exp2f(-hb[Q + 1][i0]);
+  }
+}
+
+template <int T, int NOUT, int Q, int m>
+__device__ __forceinline__ void x3_slot_f(const char* lb, floatx16 (&hb)[T], floatx16 (&acc)[NOUT],
+                                          halfx8 (&fr)[2][2], halfx8 (&cs)[2], halfx8 (&s1)[2], uint32_t (&s1h)[4],
+                                          float (&tq)[5], uint32_t (&nh)[8], uint32_t (&nl)[8], float c) {
+  constexpr int t = m / 3, j = m % 3, ks = t / NOUT, o = t % NOUT;
+  if constexpr (j == 0 && t + 1 < 2 * NOUT) load_frag<2>(lb + (((t + 1) * 2) << 10), fr[(t + 1) & 1]);
+  if constexpr (ks == 0) acc[o] = mfma_term2(fr[t & 1], cs, j, acc[o]);
+  else acc[o] = mfma_term2(fr[t & 1], s1, j, acc[o]);
+  x3_valu_slot_f<T, NOUT, Q, m>(hb, s1, s1h, tq, nh, nl, c);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int T, int NOUT, int Q, int... M>
+__device__ __forceinline__ void x3_slots_all_f(std::integer_sequence<int, M...>, const char* lb, floatx16 (&hb)[T],
+                                               floatx16 (&acc)[NOUT], halfx8 (&fr)[2][2], halfx8 (&cs)[2],
+                                               halfx8 (&s1)[2], uint32_t (&s1h)[4], float (&tq)[5],
+                                               uint32_t (&nh)[8], uint32_t (&nl)[8], float c) {
+  (x3_slot_f<T, NOUT, Q, M>(lb, hb, acc, fr, cs, s1, s1h, tq, nh, nl, c), ...);
+}
+
+template <int T, int NOUT, int Q, int... M>
+__device__ __forceinline__ void x3_valu_tail_f(std::integer_sequence<int, M...>, floatx16 (&hb)[T], halfx8 (&s1)[2],
+                                               uint32_t (&s1h)[4], float (&tq)[5], uint32_t (&nh)[8],
+                                               uint32_t (&nl)[8], float c) {
+  (x3_valu_slot_f<T, NOUT, Q, 2 * NOUT * 3 + M>(hb, s1, s1h, tq, nh, nl, c), ...);
+}
+
+// x3_step_slots with the fused swish + split: cs / s1 hold tile Q's k-step
+// 0 / 1 terms (s1 formed here for Q == 0), and leave tile Q+1's.
+template <int T, int NOUT, int Q, bool HASB>
+__device__ __forceinline__ void x3_step_slots_f(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                                floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                                int hh, halfx8 (&cs)[2], halfx8 (&s1)[2], float isc, float us) {
+  constexpr int NT = 2;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+  const char* lb = p.cur + lane * 16;
+  halfx8 fr[2][NT];
+  load_frag<NT>(lb, fr[0]);
+  constexpr int kSlots = 2 * NOUT * 3;
+  float tq[5];
+  uint32_t s1h[4], nh[8], nl[8];
+  x3_slots_all_f<T, NOUT, Q>(std::make_integer_sequence<int, kSlots>{}, lb, hb, acc, fr, cs, s1, s1h, tq, nh, nl,
+                             isc);
+  x3_valu_tail_f<T, NOUT, Q>(std::make_integer_sequence<int, (kSlots < 21 ? 21 - kSlots : 0)>{}, hb, s1, s1h, tq,
+                             nh, nl, isc);
+  if constexpr (HASB) {
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bias_acc(bias + o * 32, hh));
+  }
+  if constexpr (Q + 1 < T) {
+    __builtin_memcpy(&cs[0], &nh[0], 16);
+    __builtin_memcpy(&cs[1], &nl[0], 16);
+    __builtin_memcpy(&s1[0], &nh[4], 16);
+    __builtin_memcpy(&s1[1], &nl[4], 16);
+  }
+  char* const t = p.cur;
+  p.cur = p.nxt;
+  p.nxt = t;
+  p.g += 1;
+}
+
 // Dim-pair last layer (PAIRS, f16x2): the layer input is split once, before
 // the pair loop (sp[tile][k-step] = hi / lo), so each pair's group steps are
 // MFMAs and fragment reads only (the plain steps re-split every tile per
@@ -923,16 +1195,32 @@ __device__ __forceinline__ void x3_layer_pre(const char* __restrict__ x3, X3Pipe
 template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
-                                              typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
+                                              typename XT<NT>::E (&cs)[NT], float isc, float us, int act,
+                                              halfx8 (&fused_s1)[2]) {
 #if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
 #define X3_STEP x3_step_up
 #else
 #define X3_STEP x3_step_pipe
 #endif
+#ifndef ZF_X3_FUSED
+#define ZF_X3_FUSED 0
+#endif
+  if constexpr (NT == 2 && !OACT && ZF_X3_FUSED) {  // the swish kernels, fused swish + split
+    static_assert(sizeof(typename XT<NT>::E) == 16, "halfx8 terms");
+    halfx8(&s1)[2] = fused_s1;
+    if constexpr (Q + 1 < T) {
+      x3_step_slots_f<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, s1, isc, us);
+      x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act, s1);
+    } else {
+      x3_step_slots_f<T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, s1, isc, us);
+    }
+    return;
+  }
   if constexpr (NT == 2 && !OACT) {  // the swish kernels: explicit MFMA slots (x3_step_slots)
     if constexpr (Q + 1 < T) {
       x3_step_slots<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us);
-      x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
+      x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act,
+                                                    fused_s1);
     } else {
       x3_step_slots<T, NOUT, Q, HASB>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us);
     }
@@ -940,11 +1228,27 @@ __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pip
   }
   if constexpr (Q + 1 < T) {
     X3_STEP<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
-    x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
+    x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act, fused_s1);
   } else {
     X3_STEP<NT, T, NOUT, Q, HASB, OACT>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   }
 #undef X3_STEP
+}
+
+// A layer of the early-scale path (f16x2 swish, hidden 128): steps 0..T-2 as
+// x3_step_slots (the layer input's tiles 1..T-1 swished with c in their
+// slots), then x3_step_slots_last (finish; NEXT: the next layer's tile 0
+// swished with cn and split into cs).
+template <int T, int NOUT, bool NEXT, int SPT = 0, int Q = 0>
+__device__ __forceinline__ void x3_layer_early(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
+                                               floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
+                                               int hh, halfx8 (&cs)[2], float c, float us, float cn, float& mx) {
+  if constexpr (Q + 1 < T) {
+    x3_step_slots<T, NOUT, Q, false>(x3, p, hb, acc, lane, nullptr, hh, cs, c, us);
+    x3_layer_early<T, NOUT, NEXT, SPT, Q + 1>(x3, p, hb, acc, lane, bias, hh, cs, c, us, cn, mx);
+  } else {
+    x3_step_slots_last<T, NOUT, NEXT, SPT>(x3, p, hb, acc, lane, bias, hh, cs, us, cn, mx);
+  }
 }
 
 // A whole streamed Dense layer: T groups (one per input tile).
@@ -967,7 +1271,8 @@ __device__ __forceinline__ void x3_layer(const char* __restrict__ x3, X3Pipe& p,
 // the weight-group DMA in flight.
 template <int T, bool OACT>
 __device__ __forceinline__ void x3_layer0(const X3Sc& c, const float* par, const float* xs, int rot, int D,
-                                          int s, int hh, int lane, floatx16 (&hb)[T], int swish_tiles) {
+                                          int s, int hh, int lane, floatx16 (&hb)[T], int swish_tiles,
+                                          float* umax = nullptr) {
   const int dt = c.dt, dc = c.dc, DC = c.DC, KS0 = c.KS0;
   const int DCp = 2 * KS0;
   const float* bn = par;
@@ -981,6 +1286,7 @@ __device__ __forceinline__ void x3_layer0(const X3Sc& c, const float* par, const
     if (k < dc) v = xs[wrap(dt + k + rot, D) * 32 + s];
     else if (k < DC) v = xs[(D + k - dc) * 32 + s];
     const float u = (v - bn[k]) * bn[DCp + k] + bn[2 * DCp + k];
+    if (umax != nullptr) *umax = fmaxf(*umax, fabsf(u));  // padding inputs are 0: bn rows give u = 0
     const float* w0 = w0b + ks * 64 + lane;
 #pragma unroll
     for (int o = 0; o < T; ++o) hb[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(w0[o * KS0 * 64], u, hb[o], 0, 0, 0);
@@ -1056,6 +1362,111 @@ __device__ __forceinline__ float x3_squareplus_t(float x) {
   return 0.5f * (x + (CR ? x3_sqrt_cr(a) : __builtin_amdgcn_sqrtf(a)));
 }
 
+// Bin selection over a power-of-two number of bins N by halving (log2 N
+// compares, each followed by selects of the upper or lower half): bins
+// base..base+N-1 have left knots X / Y, raw widths Wd / heights Ht and knot
+// slope logits S (N + 1: both ends of every bin).  For strictly increasing
+// knots this is the last bin whose left knot is <= v (and bin 0 for v below
+// knot 1, or NaN): the same bin as the linear sweep of rqs_bin_monotone, with
+// 4 compares and 79 selects at K = 16 instead of 15 and 90.
+template <bool FWD, int N, int MX>
+__device__ __forceinline__ void x3_bsel(float v, const float (&X)[MX], const float (&Y)[MX], const float (&Wd)[N],
+                                        const float (&Ht)[N], const float (&S)[N + 1], float (&out)[6]) {
+  static_assert(MX >= N, "knot arrays cover the bins");
+  if constexpr (N == 1) {
+    out[0] = X[0]; out[1] = Y[0]; out[2] = Wd[0]; out[3] = Ht[0]; out[4] = S[0]; out[5] = S[1];
+  } else {
+    constexpr int H = N / 2;
+    const bool c = (FWD ? X[H] : Y[H]) <= v;
+    float X2[H], Y2[H], W2[H], H2[H], S2[H + 1];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      X2[i] = c ? X[H + i] : X[i];
+      Y2[i] = c ? Y[H + i] : Y[i];
+      W2[i] = c ? Wd[H + i] : Wd[i];
+      H2[i] = c ? Ht[H + i] : Ht[i];
+    }
+#pragma unroll
+    for (int i = 0; i <= H; ++i) S2[i] = c ? S[H + i] : S[i];
+    x3_bsel<FWD, H, H>(v, X2, Y2, W2, H2, S2, out);
+  }
+}
+
+// softmax_with_threshold's constants for a compile-time knot count (the
+// kernel's K equals the couplings' real K): c * rnorm * j as literals.
+template <int K>
+struct KnotLit {
+  static constexpr double c64 = 1e-5 / (1.0 - (double)K * 1e-5);
+  static constexpr float c = (float)c64;
+  static constexpr float norm = (float)(1.0 + c64 * (double)K);
+  static constexpr float rnorm = (float)(1.0 / (double)norm);
+  static constexpr float bc = c * rnorm;
+};
+
+// normalize_spline_params (utils.py:37-62) + the bin gather of
+// _compute_rqs_input (utils.py:205-232) for one (sample, dim) per lane, from
+// the raw logits P (widths P[0..K), heights P[K..2K), inner slopes
+// P[2K..3K-1)).  With s_j = 2 squareplus(logit_j) (the factor 1/2 cancels in
+// the quotient) and S = sum s_j, the normalised width is w_j = s_j a + bc
+// (a = rnorm / S, bc = c rnorm: one fma, as before) and knot j is
+// X_j = W_j a + j bc, W_j = s_0 + ... + s_{j-1} the raw running sum, which
+// the normalisation forms anyway (its last term is S): one fma per knot
+// instead of a normalising fma plus a running add.  The knots round
+// differently from the reference's cumsum of normalised widths in the last
+// ulp (as the fma'd widths already did); the spline is continuous across
+// knots.  KLIT: j bc as literals (the kernel's K is the couplings' K); else
+// from the runtime constants (padded knot counts).  Bin: x3_bsel; v at or
+// beyond the last knot gives the idx == K fill (NaN width, height and right
+// slope, utils.py:224-230) as rqs_bin_monotone.
+template <bool FWD, int K, bool CR, bool KLIT, int NPV>
+__device__ __forceinline__ RqsBin x3_bin(float v, const float (&P)[NPV], const KnotConsts& kc) {
+  float ws[K], hs[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    ws[j] = x3_squareplus2_t<CR>(P[j]);
+    hs[j] = x3_squareplus2_t<CR>(P[K + j]);
+  }
+  float X[K + 1], Y[K + 1];  // raw running sums, then knots
+  X[0] = 0.f;
+  Y[0] = 0.f;
+  X[1] = ws[0];
+  Y[1] = hs[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    X[j + 1] = X[j] + ws[j];
+    Y[j + 1] = Y[j] + hs[j];
+  }
+  const float rn = KLIT ? KnotLit<K>::rnorm : kc.rnorm;
+  const float bc = KLIT ? KnotLit<K>::bc : kc.c * kc.rnorm;
+  const float ax = rcp_refined(X[K]) * rn, ay = rcp_refined(Y[K]) * rn;
+#pragma unroll
+  for (int j = 1; j <= K; ++j) {
+    const float jb = KLIT ? (float)j * KnotLit<K>::bc : (float)j * bc;
+    X[j] = __builtin_fmaf(X[j], ax, jb);
+    Y[j] = __builtin_fmaf(Y[j], ay, jb);
+  }
+  float S[K + 1];
+  S[0] = 0.f;  // the boundary derivative 1 as the logit 0 (squareplus(0) == 1)
+  S[K] = 0.f;
+#pragma unroll
+  for (int j = 1; j < K; ++j) S[j] = P[2 * K + j - 1];
+  float o[6];
+  x3_bsel<FWD, K, K + 1>(v, X, Y, ws, hs, S, o);
+  RqsBin b;
+  const bool sliver = (FWD ? X[K] : Y[K]) <= v;
+  b.xk = sliver ? X[K] : o[0];
+  b.yk = sliver ? Y[K] : o[1];
+  b.w = sliver ? qnan() : __builtin_fmaf(o[2], ax, bc);
+  b.h = sliver ? qnan() : __builtin_fmaf(o[3], ay, bc);
+  const float lo = sliver ? 0.f : o[4];
+  const float hi = sliver ? qnan() : o[5];
+  b.dk = lo == 0.f ? 1.f : x3_squareplus_t<CR>(lo);
+  b.dkp1 = hi == 0.f ? 1.f : x3_squareplus_t<CR>(hi);
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+
 // Block: 4 waves x 32 samples, one 32-row input tile per weight group,
 // double-buffered in LDS.  Small parameters (BatchNorm, first Dense, biases,
 // ShiftBounds rows) are read from global memory (L2-resident), so the LDS
@@ -1080,7 +1491,7 @@ constexpr int x3_occupancy() { return T == 8 ? 1 : 2; }
 constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
 #endif
 
-template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT>
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT, int ASET = 0>
 __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
     const DevFlow* __restrict__ F, const float* __restrict__ blob, const char* __restrict__ x3,
     const float* __restrict__ xin, const float* __restrict__ cin, float* __restrict__ y_out,
@@ -1137,8 +1548,16 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
     tacc[k] += t_ - t_last;                      \
     t_last = t_;                                 \
   }
+#elif defined(ZF_X3_MARK)
+  // tuning only: phase markers in the .s for per-phase static instruction counts
+#define X3T(k) asm volatile(";ZFMARK " #k)
 #else
 #define X3T(k)
+#endif
+#ifdef ZF_X3_MARK
+#define X3M(k) asm volatile(";ZFMARK " #k)
+#else
+#define X3M(k)
 #endif
   pipe.par_src = nullptr;
   pipe.par_dst = nullptr;
@@ -1162,6 +1581,11 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   int nsc_i = 0;  // NSCs entered, in execution order: parameter region nsc_i & 1
 
   const KnotConsts kc(F->kreal);  // the couplings' knots (K may be padded above them)
+#ifdef ZF_X3_MARK
+  const bool klit = true;  // marker builds: count one x3_bin copy
+#else
+  const bool klit = F->kreal == K;  // x3_bin: the knot constants as literals
+#endif
   const int nq = op_end - op_begin;
   for (int q = 0; q < nq; ++q) {
     const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
@@ -1201,7 +1625,31 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // layer scales and swishes them (act_swish) as it goes.
       // bf16x3 OACT: every tile's activation at the layer end (no switch inside
       // the group steps)
-      x3_layer0<T, OACT>(opc, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (!OACT && (nh > 1 || kLastSW)) ? 1 : T);
+#ifndef ZF_X3_EARLY
+#define ZF_X3_EARLY 1
+#endif
+      // f16x2 swish at hidden 128 (one dim pair): scales from bounds (x3_early_scale)
+      constexpr bool kEarly = ZF_X3_EARLY && NT == 2 && !OACT && kPipe;
+      // kEarly: the last layer's width / height tiles leave its last group
+      // step as 2 squareplus (x3_step_slots_last SPT): K / 8 tiles of 16 per
+      // lane half (one dim per half); ONE at K = 16: tile 0 (widths on half 0,
+      // heights on half 1, the kSplitWH layout)
+#ifndef ZF_X3_PRESP
+#define ZF_X3_PRESP 1
+#endif
+      constexpr int kPreSP = (!ZF_X3_PRESP || !kEarly) ? 0 : !ONE ? K / 8 : (K == 16 ? 1 : 0);
+      float umax = 0.f;
+      x3_layer0<T, OACT>(opc, par, xs, rot, D, s, hh, lane, hb, NT == 2 ? 0 : (!OACT && (nh > 1 || kLastSW)) ? 1 : T,
+                         kEarly ? &umax : nullptr);
+      float eU = 0.f, eisc = 1.f, eus = 1.f, eius = 1.f;  // kEarly: bound and scales of the current layer input
+      halfx8 ecs[2];  // kEarly: k-step-0 split of the current layer input's tile 0
+      if constexpr (kEarly) {
+        umax = fmaxf(umax, __shfl_xor(umax, 32));
+        eU = __builtin_fmaf(op.x3_rb[0][0], umax, op.x3_rb[0][1]);
+        x3_scale_from(eU, nh > 1 ? opc.kw1 : kw_last, eisc, eus, eius);
+        x3_act_tile<NT, false>(hb[0], eisc, act);
+        split8h<0>(hb[0], ecs[0], ecs[1]);
+      }
       // Hidden layers 1..n_hidden-1 (:343-345), T groups each.  bf16x3: the
       // biases seed the accumulators.  f16x2: they seed them divided by the
       // unscale (exact: powers of two) and the accumulators are multiplied
@@ -1234,6 +1682,26 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       if constexpr (T == 4) __builtin_amdgcn_s_setprio(2);
 #endif
       X3T(1);
+      if constexpr (kEarly) {
+        float eM = eU;  // max |v'| of the current layer input's pre-activations (exact from layer 2 on)
+        for (int l = 1; l < nh; ++l) {
+          // the next layer's input bound and scales (its tile 0 is swished in this layer's last
+          // step), from the exact maximum of this layer's input, so bounds never compound
+          const float nU = __builtin_fmaf(op.x3_rb[l][0], eM, op.x3_rb[l][1]);
+          float nisc, nus, nius;
+          x3_scale_from(nU, l + 1 < nh ? op.x3_kw[l + 1] : kw_last, nisc, nus, nius);
+          floatx16 acc[T];
+#pragma unroll
+          for (int o = 0; o < T; ++o) acc[o] = floatx16{0};
+          float mx;
+          x3_layer_early<T, T, true>(x3, pipe, hb, acc, lane, par + b_rel + (l - 1) * (T * 32), hh, ecs, eisc, eus,
+                                     nisc, mx);
+#pragma unroll
+          for (int o = 0; o < T; ++o) hb[o] = acc[o];
+          eU = nU; eisc = nisc; eus = nus; eius = nius;
+          eM = fmaxf(mx, __shfl_xor(mx, 32));
+        }
+      } else
       for (int l = 1; l < nh; ++l) {
         floatx16 acc[T];
         float isc = 1.f, us = 1.f, ius = 1.f;
@@ -1242,7 +1710,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           // OACT: every tile here, outside the MFMA stream (the switch there
           // would cost a third of the waves)
 #pragma unroll
-          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT>(hb[o], isc, act);
+          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT, ASET>(hb[o], isc, act);
         }
         const float* bl_l = par + b_rel + (l - 1) * (T * 32);
 #pragma unroll
@@ -1253,8 +1721,9 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         if constexpr (kPipeH) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
+          halfx8 fs1[2];  // ZF_X3_FUSED: the k-step 1 terms carried between group steps
           x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaledH, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
-                                                                 act);
+                                                                 act, fs1);
         } else {
           x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, act);
         }
@@ -1286,12 +1755,14 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // dead once the last layer has consumed them.
       const int npair = PAIRS ? (dt + 1) / 2 : 1;
       float lisc = 1.f, lus = 1.f, lius = 1.f;  // f16x2 scales of the last layer's input (all pairs)
-      if constexpr (NT == 2) {
+      if constexpr (kEarly) {
+        lisc = eisc; lus = eus; lius = eius;  // tile 0 swished, ecs its split
+      } else if constexpr (NT == 2) {
         x3_act_scale<T, OACT>(hb, kw_last, lisc, lus, lius, act);
         // PAIRS: the input is read once per dim pair, so swish it whole here
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT>(hb[o], lisc, act);
+          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT, ASET>(hb[o], lisc, act);
       }
 #ifndef ZF_X3_PRESPLIT
 #define ZF_X3_PRESPLIT 1
@@ -1320,12 +1791,16 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         for (int o = 0; o < TL; ++o)
           pa[o] = kSeed ? bias_acc(bl + o * 32, hh) : (kSeedScaled ? bias_acc(bl + o * 32, hh) * lius : floatx16{0});
         X3T(3);
-        if constexpr (kPre) {
+        if constexpr (kEarly) {
+          float mx;
+          x3_layer_early<T, TL, false, kPreSP>(x3, pipe, hb, pa, lane, bl, hh, ecs, lisc, lus, 0.f, mx);
+        } else if constexpr (kPre) {
           x3_layer_pre<T, TL>(x3, pipe, sp, pa, lane);
         } else if constexpr (kPipe) {
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
-          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, act);
+          halfx8 fs1[2];
+          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, act, fs1);
         } else {
           x3_layer<NT, T, TL, kLastSW, OACT>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh,
                                              lisc, lus, act);
@@ -1361,55 +1836,74 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
               P[16 * o + r] = pa[o][r];
             }
           }
+        X3M(11);
+#if ZF_X3_ABL == 10 || ZF_X3_ABL == 11  // tuning: 64 extra VALU (10: v_add, 11: v_exp) in the spline phase
+#pragma unroll
+        for (int q2 = 0; q2 < 64; ++q2) {
+          float dd;
+          if (ZF_X3_ABL == 10) asm volatile("v_add_f32 %0, %1, %2" : "=v"(dd) : "v"(pa[0][q2 & 15]), "v"(pa[1][q2 & 15]));
+          else asm volatile("v_exp_f32 %0, %1" : "=v"(dd) : "v"(pa[0][q2 & 15]));
+        }
+#endif
         // normalize_spline_params (utils.py:37-62) + RQ spline (utils.py:65-250)
         const int d = 2 * pr + hh;
         const bool dact = d < dt;  // the upper half idles on an odd last dim
         float ldv = 0.f;
         {
-          float w[K], hg[K];
-          const float bc = kc.c * kc.rnorm;
-          if constexpr (kSplitWH) {
-            float sw = 0.f;  // half 0: the widths' sum, half 1: the heights'
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-              w[j] = x3_squareplus2_t<OACT>(P[j]);
-              sw = sw + w[j];
-            }
-            const float a = rcp_refined(sw) * kc.rnorm;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-              const float f = __builtin_fmaf(w[j], a, bc);
-              const float other = __shfl_xor(f, 32);
-              w[j] = hh == 0 ? f : other;
-              hg[j] = hh == 0 ? other : f;
-            }
-          } else {
-            float sx = 0.f, sy = 0.f;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
-              w[j] = x3_squareplus2_t<OACT>(P[j]);
-              hg[j] = x3_squareplus2_t<OACT>(P[K + j]);
-              sx = sx + w[j];
-              sy = sy + hg[j];
-            }
-            // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
-            // 2*squareplus: the same quotient bits): the parameters
-            // themselves already differ from the reference's in the last ulp
-            // (GEMM summation order), so correctly rounded divisions buy nothing.
-            const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-              w[j] = __builtin_fmaf(w[j], ax, bc);
-              hg[j] = __builtin_fmaf(hg[j], ay, bc);
-            }
-          }
-          float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
-#pragma unroll
-          for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
           float* xp = xs + wrap((dact ? d : 0) + rot, D) * 32 + s;
           const float xv = *xp;
-          const RqsBin bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
-                                                       [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); });
+#ifndef ZF_X3_BSEARCH
+#define ZF_X3_BSEARCH 0
+#endif
+          RqsBin bin;
+          if constexpr (ZF_X3_BSEARCH && !kSplitWH && (K == 8 || K == 16 || K == 32)) {
+            bin = klit ? x3_bin<!INV, K, OACT, true>(xv, P, kc) : x3_bin<!INV, K, OACT, false>(xv, P, kc);
+          } else {
+            float w[K], hg[K];
+            const float bc = kc.c * kc.rnorm;
+            if constexpr (kSplitWH) {
+              float sw = 0.f;  // half 0: the widths' sum, half 1: the heights'
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                w[j] = kPreSP ? P[j] : x3_squareplus2_t<OACT>(P[j]);
+                sw = sw + w[j];
+              }
+              const float a = rcp_refined(sw) * kc.rnorm;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                const float f = __builtin_fmaf(w[j], a, bc);
+                const float other = __shfl_xor(f, 32);
+                w[j] = hh == 0 ? f : other;
+                hg[j] = hh == 0 ? other : f;
+              }
+            } else {
+              float sx = 0.f, sy = 0.f;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {  // squareplus + sums in order (utils.py:30-33)
+                w[j] = kPreSP ? P[j] : x3_squareplus2_t<OACT>(P[j]);
+                hg[j] = kPreSP ? P[K + j] : x3_squareplus2_t<OACT>(P[K + j]);
+                sx = sx + w[j];
+                sy = sy + hg[j];
+              }
+              // (v / sum + c) / (1 + c K) as one fma per knot (v and sum both
+              // 2*squareplus: the same quotient bits): the parameters
+              // themselves already differ from the reference's in the last ulp
+              // (GEMM summation order), so correctly rounded divisions buy nothing.
+              const float ax = rcp_refined(sx) * kc.rnorm, ay = rcp_refined(sy) * kc.rnorm;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                w[j] = __builtin_fmaf(w[j], ax, bc);
+                hg[j] = __builtin_fmaf(hg[j], ay, bc);
+              }
+            }
+            X3M(12);
+            float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
+#pragma unroll
+            for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
+            bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
+                                                         [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); });
+            X3M(13);
+          }
           float yv;
           if (!INV) {
             float l;
@@ -1445,9 +1939,10 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   }
 #endif
 #undef X3T
+#undef X3M
 }
 
-template <int NT, int K, int T, bool PAIRS, bool ONE, bool OACT>
+template <int NT, int K, int T, bool PAIRS, bool ONE, bool OACT, int ASET = 0>
 int launch_x3(const X3Launch& a, bool inverse) {
   const long long rows = kX3Waves * kTile;
   const long long grid = (a.N + rows - 1) / rows;
@@ -1460,11 +1955,11 @@ int launch_x3(const X3Launch& a, bool inverse) {
 #endif
   if (lds > 160 * 1024) return enotsup("bf16x3 LDS footprint too large");
   if (inverse)
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true, OACT>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, true, OACT, ASET>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   else
-    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false, OACT>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
+    hipLaunchKernelGGL((flow_kernel_x3<NT, K, T, PAIRS, ONE, false, OACT, ASET>), dim3((unsigned)grid), dim3(kX3Waves * 64), lds, a.stream,
                        a.desc, a.blob, (const char*)a.x3, a.x, a.c, a.y, a.ld_in, a.ld_out, a.lp, a.part,
                        a.nparts, a.op_begin, a.op_end, a.N, a.seed, a.gen);
   ZF_CHECK_LAUNCH("flow_kernel_x3");
@@ -1476,17 +1971,18 @@ int launch_x3(const X3Launch& a, bool inverse) {
 // last layer) whenever dt > 2, and always at T = 8 (its hidden activations
 // are live across the last layer anyway); ONE when dt == 1.
 // OACT: some coupling's activation is not swish (f16x2 only).
-template <int NT, int K, bool OACT = false>
+template <int NT, int K, bool OACT = false, int ASET = 0>
 int launch_x3_k(const X3Launch& a, bool inverse) {
   const int dt = a.D / 2;
   const bool one = dt == 1;  // must match x3_pack's last-layer layout
   if (a.T == 4) {
-    if (dt > 2) return launch_x3<NT, K, 4, true, false, OACT>(a, inverse);
-    return one ? launch_x3<NT, K, 4, false, true, OACT>(a, inverse)
-               : launch_x3<NT, K, 4, false, false, OACT>(a, inverse);
+    if (dt > 2) return launch_x3<NT, K, 4, true, false, OACT, ASET>(a, inverse);
+    return one ? launch_x3<NT, K, 4, false, true, OACT, ASET>(a, inverse)
+               : launch_x3<NT, K, 4, false, false, OACT, ASET>(a, inverse);
   }
   if (a.T == 8)
-    return one ? launch_x3<NT, K, 8, true, true, OACT>(a, inverse) : launch_x3<NT, K, 8, true, false, OACT>(a, inverse);
+    return one ? launch_x3<NT, K, 8, true, true, OACT, ASET>(a, inverse)
+               : launch_x3<NT, K, 8, true, false, OACT, ASET>(a, inverse);
   return enotsup("split-MFMA kernel: hidden tiles not instantiated");
 }
 

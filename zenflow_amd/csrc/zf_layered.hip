@@ -23,6 +23,7 @@
 #include "zf_flow_dev.h"
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 namespace zf {
@@ -35,6 +36,11 @@ struct LayeredFlow {
         *P = nullptr;
   void* block = nullptr;  // one allocation holding the buffers above
   int hmax = 1, dcmax = 1, outmax = 1;
+  // One call at a time per handle: layered_run may grow (free + reallocate)
+  // the workspace above, and every launch of a call reads its pointers, so
+  // a second host thread on the same handle waits until the first has
+  // enqueued all its launches (hipFree then waits for them on the device).
+  std::mutex mu;
 };
 
 namespace {
@@ -179,9 +185,12 @@ int layered_run(LayeredFlow* L, const DevFlow& F, const float* packed, bool inve
                 long long N, hipStream_t st, unsigned long long seed, int gen) {
   const zf_flow_desc& desc = L->desc;
   const int D = desc.dim, C = desc.cond_dim;
-  // rows per chunk: a multiple of the 128-row NLL partial, each hidden
-  // activation buffer within kChunkFloats
-  long long R = std::max(128ll, (kChunkFloats / L->hmax) / 128 * 128);
+  std::lock_guard<std::mutex> lock(L->mu);
+  // rows per chunk: a multiple of the 128-row NLL partial, every buffer of
+  // the workspace (hidden activations, the conditioner input U, the spline
+  // parameters P) within kChunkFloats, so each GEMM's M * N stays below 2^26
+  const long long wmax = std::max<long long>({L->hmax, L->outmax, L->dcmax});
+  long long R = std::max(128ll, (kChunkFloats / wmax) / 128 * 128);
   R = std::min(R, (N + 127) / 128 * 128);
   int rc = ensure_rows(L, R);
   if (rc) return rc;

@@ -546,7 +546,8 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
   if (big >= 512 && !tb && K <= 8) {
     // the first Dense (K = dc + C <= 8) at large batches too: one thread per
     // output is bound by its Z / H stores, the MFMA tiles would multiply a
-    // 32-deep k-tile of zeros (the choice follows the global batch, as below)
+    // 32-deep k-tile of zeros (the choice follows the global batch, as below;
+    // not a split-set form, so ZF_TRAIN_SPLITQ=0 keeps it)
     const long long MN = (long long)M * N;
     hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
                        ldb, C, ldc, epi, bias, H, Z, act);

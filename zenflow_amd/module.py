@@ -221,9 +221,25 @@ class _SetupRef:
         self.kind, self.args = kind, args
 
     def resolve(self, module):
-        if self.kind == "param":
-            return Module.param(module, *self.args)
-        return Module.variable(module, *self.args)
+        d = module.__dict__
+        in_setup = d.get("_zf_in_setup")
+        if in_setup:
+            # setup() reading a variable it has just declared (flax allows
+            # `self.w = self.param(...); n = self.w.shape[0]`): resolve it
+            # against the init/apply call that triggered setup()
+            if getattr(_tls, "scope", None) is None:
+                raise RuntimeError(
+                    f"{type(module).__name__}.setup() reads {self.kind} {self.args[0]!r} outside init/apply: "
+                    "variables declared in setup() have values only inside module.init / module.apply"
+                )
+            d["_zf_in_setup"] = False
+        try:
+            if self.kind == "param":
+                return Module.param(module, *self.args)
+            return Module.variable(module, *self.args)
+        finally:
+            if in_setup:
+                d["_zf_in_setup"] = True
 
     def __repr__(self):
         return f"<{self.kind} {self.args[0]!r} declared in setup()>"
@@ -311,11 +327,11 @@ class Module:
 
         gen = as_generator(rng)
         if type(self)._init_variables is Module._init_variables:
-            self._ensure_setup()
             scope = Scope({}, True, owner=self, initializing=True, rng=gen)
             prev = getattr(_tls, "scope", None)
             _tls.scope = scope
             try:
+                self._ensure_setup()  # inside the scope: setup() may read what it declares
                 _resolve_method(self, method)(self, *args, **kwargs)
             finally:
                 _tls.scope = prev
@@ -342,12 +358,12 @@ class Module:
 
         With ``mutable`` (e.g. ``["batch_stats"]``) returns ``(out, updates)``
         as FLAX does."""
-        self._ensure_setup()
         fn = _resolve_method(self, method)
         scope = Scope(variables, mutable, owner=self)
         prev = getattr(_tls, "scope", None)
         _tls.scope = scope
         try:
+            self._ensure_setup()  # inside the scope: setup() may read what it declares
             out = fn(self, *args, **kwargs)
         finally:
             _tls.scope = prev
