@@ -238,14 +238,18 @@ def oracle_spec(name):
 
 
 def load_pmc(kernel_prefix):
-    """The committed PMC summary of the headline kernel (profiles/pmc_traffic.json,
-    written by scripts/summarize_profiles.py from rocprofv3 passes over this
-    bench): HBM bytes per launch and the MFMA / VALU pipe fractions, or {}."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    try:
-        return json.loads(f.read_text()).get(kernel_prefix, {})
-    except (OSError, ValueError):
-        return {}
+    """The committed PMC summaries of the headline kernel: HBM bytes per
+    launch (profiles/pmc_traffic.json, scripts/summarize_profiles.py over
+    FETCH_SIZE / WRITE_SIZE passes of this bench) and the matrix / vector
+    pipe fractions (profiles/x3_pipe_counters.json, scripts/summarize_stall.py
+    over the SQ passes of scripts/pmc_stall.sh), or {}."""
+    out = {}
+    for fname in ("pmc_traffic.json", "x3_pipe_counters.json"):
+        try:
+            out.update(json.loads((ROOT / "profiles" / fname).read_text()).get(kernel_prefix, {}))
+        except (OSError, ValueError):
+            pass
+    return out
 
 
 def make_workload(name, N, rank=0):
@@ -551,7 +555,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if variant not in SPLIT_PEAKS else f"fp32 ({variant} split MFMA, fp32 accumulate)",
         "data": "synthetic: x ~ N(0, I) per rank; random-init weights (flax default initialisers) "
                 "+ one train-mode pass for ShiftBounds/BatchNorm statistics",
         "config": dict(run_config(name, N, world), kernel=variant),
@@ -571,6 +575,7 @@ def main():
             "valu_active": pmc.get("valu_active"),
             "valu_mfma_coexec": pmc.get("valu_mfma_coexec"),
             "pmc_source": pmc.get("source"),
+            "pipe_source": pmc.get("pipe_source"),
             "pmc_grid": pmc.get("grid"),
         },
     }

@@ -43,6 +43,18 @@ CONFIGS = {
     "k15": dict(D=4, C=0, K=15, layers=(128, 128), latent="normal"),
     "k24h256": dict(D=6, C=0, K=24, layers=(256, 256), latent="normal", couplings=3),
     "k3": dict(D=2, C=0, K=3, layers=(64, 64), latent="normal"),
+    # round 5: one padded knot (K = 7 / 15 / 31 on the 8 / 16 /
+    # 32 instantiations: the sliver starts at the padded knot), 33..64 knots on the
+    # K = 64 instantiation (one wave per SIMD), knots above 64 on the layered
+    # path, and a chain mixing knot counts (every coupling at the largest one's
+    # instantiation, each with its own knot constants)
+    "k7": dict(D=4, C=0, K=7, layers=(128, 128), latent="normal"),
+    "k31": dict(D=4, C=0, K=31, layers=(128, 128), latent="normal"),
+    "k40": dict(D=4, C=0, K=40, layers=(128, 128), latent="normal"),
+    "k64": dict(D=4, C=0, K=64, layers=(128, 128), latent="normal"),
+    "k64c1": dict(D=3, C=1, K=64, layers=(128, 128), latent="beta"),
+    "k100": dict(D=4, C=0, K=100, layers=(128, 128), latent="normal"),
+    "kmix": dict(D=4, C=0, K=(16, 8, 31, 12), layers=(128, 128), latent="normal"),
     # NeuralSplineCoupling(act=...) other than swish (bijectors.py:319): the
     # split-MFMA kernel's activation switch (sigmoid / softplus: the fp32
     # kernel) and the trainer
@@ -67,15 +79,16 @@ ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu", "mix
 
 
 def chain_spec(cfg):
-    D, K, layers = cfg["D"], cfg["K"], list(cfg["layers"])
+    D, layers = cfg["D"], list(cfg["layers"])
     L = cfg.get("couplings", D)
     acts = cfg.get("act", "swish")
     acts = [acts] if isinstance(acts, str) else list(acts)  # a list: one per coupling, cycled
+    ks = cfg["K"] if isinstance(cfg["K"], (tuple, list)) else (cfg["K"],)  # likewise knots
     bij = [{"type": "shift_bounds", "margin": cfg.get("margin", 0.1), "bounds": cfg.get("bounds", ())}]
     for i in range(L - 1):
-        bij.append({"type": "nsc", "knots": K, "layers": layers, "act": acts[i % len(acts)]})
+        bij.append({"type": "nsc", "knots": ks[i % len(ks)], "layers": layers, "act": acts[i % len(acts)]})
         bij.append({"type": "roll", "shift": 1})
-    bij.append({"type": "nsc", "knots": K, "layers": layers, "act": acts[(L - 1) % len(acts)]})
+    bij.append({"type": "nsc", "knots": ks[(L - 1) % len(ks)], "layers": layers, "act": acts[(L - 1) % len(acts)]})
     return {"type": "chain", "bijectors": bij}
 
 
@@ -86,7 +99,7 @@ def _lecun(rng, fan_in, fan_out):
 
 
 def make_variables(cfg, rng, bias_scale=0.3):
-    D, C, K = cfg["D"], cfg["C"], cfg["K"]
+    D, C = cfg["D"], cfg["C"]
     spec = chain_spec(cfg)
     dt = D // 2
     DC = D - dt + C
@@ -94,6 +107,7 @@ def make_variables(cfg, rng, bias_scale=0.3):
     for i, b in enumerate(spec["bijectors"]):
         key = f"bijectors_{i}"
         if b["type"] == "nsc":
+            K = b["knots"]
             p = {
                 "BatchNorm_0": {
                     "scale": (1 + 0.1 * rng.standard_normal(DC)).astype(np.float32),

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(1024, 1) void probe(unsigned long long* out, int it
 #pragma unroll
   for (int i = 0; i < 16; ++i) a[i] = 1.0f + 1e-3f * (lane + i) + seed;
   const float b = 0.999f + seed, c = 1e-4f;
-  const bool mfma_wave = (MODE == 3) || ((MODE != 0) && (wave < 4));  // waves 0-3 land on the 4 SIMDs
+  const bool mfma_wave = (MODE == 3) || ((MODE != 0) && (wave < 4));
+  if (MODE == 4 && mfma_wave) __builtin_amdgcn_s_setprio(3);  // waves 0-3 land on the 4 SIMDs
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   if (MODE == 0) {
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(1024, 1) void probe(unsigned long long* out, int it
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) a[r] += acc0[r] + acc1[r];
-  } else if (MODE == 2) {
+  } else if (MODE == 2 || MODE == 4) {
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
@@ -129,7 +130,8 @@ void row(unsigned long long* d, unsigned long long* h) {
   const double c4x3 = run<OP, 2, 4>(3, d, h, it) / (it * 16.0);
   const double a3 = run<OP, 3, 4>(3, d, h, it) / (it * 16.0 * 3);
   const double a3_0 = run<OP_NONE, 3, 0>(3, d, h, it) / (it * 16.0 * 3);
-  printf("  | mfma %.1f +4in %.1f +8in %.1f (1w) +4in,3w-idle %.1f +4in,2w x8 cross %.1f | 3w all mfma %.1f +4in %.1f\n", m0, m4, m8, m4x3, c4x3, a3_0, a3);
+  const double p4x3 = run<OP, 4, 4>(3, d, h, it) / (it * 16.0);
+  printf("  | mfma %.1f +4in %.1f +8in %.1f (1w) +4in,3w-idle %.1f +4in,2w x8 cross %.1f prio %.1f | 3w all mfma %.1f +4in %.1f\n", m0, m4, m8, m4x3, c4x3, p4x3, a3_0, a3);
 }
 
 int main() {
@@ -140,16 +142,7 @@ int main() {
   row<OP_MUL>(d, h);
   row<OP_EXP>(d, h);
   row<OP_RCP>(d, h);
-  row<OP_SQRT>(d, h);
   row<OP_MIX>(d, h);
-  row<OP_CVTPK>(d, h);
-  row<OP_MAX3>(d, h);
-  row<OP_CVTF16>(d, h);
-  row<OP_CVTF16HI>(d, h);
-  row<OP_AND>(d, h);
-  row<OP_LDEXP>(d, h);
-  row<OP_LOG>(d, h);
-  row<OP_MAX>(d, h);
   row<OP_CNDS>(d, h);
   return 0;
 }

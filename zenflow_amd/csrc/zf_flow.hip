@@ -353,6 +353,9 @@ int hidden_pad_of(const zf_flow_desc* desc) {
 // Widths up to 256 run in the fused kernels; wider ones on the layered path
 // (zf_layered.hip), whose row chunks shrink as the width grows.
 constexpr int kMaxFusedWidth = 256, kMaxLayeredWidth = 4096;
+// knots: the fused kernels take up to 64, the layered path's per-(row, dim)
+// spline kernels (one row's 3K - 1 parameters per thread in LDS) up to 200
+constexpr int kMaxFusedKnots = 64, kMaxLayeredKnots = 200;
 
 int validate(const zf_flow_desc* desc) {
   if (!desc) return einval("desc is NULL");
@@ -364,7 +367,8 @@ int validate(const zf_flow_desc* desc) {
     const zf_op_desc& op = desc->ops[i];
     if (op.kind == ZF_OP_NSC) {
       if (desc->dim < 2) return einval("NeuralSplineCoupling needs dim >= 2");
-      if (op.knots < 1 || op.knots > 64) return einval("knots %d out of range [1, 64]", op.knots);
+      if (op.knots < 1 || op.knots > kMaxLayeredKnots)
+        return einval("knots %d out of range [1, %d]", op.knots, kMaxLayeredKnots);
       if (op.n_hidden < 1 || op.n_hidden > 16) return enotsup("n_hidden must be in [1, 16]");
       for (int l = 0; l < op.n_hidden; ++l)
         if (op.hidden[l] < 1 || op.hidden[l] > kMaxLayeredWidth)
@@ -492,7 +496,12 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   F.n_ops = desc.n_ops;
   F.HP = zf::hidden_pad_of(&desc);
   // a conditioner wider than the fused kernels hold runs layer by layer
-  const bool layered = F.HP > zf::kMaxFusedWidth;
+  // knots beyond the fused kernels' (64: the split-MFMA kernel's largest
+  // instantiation, and the fp32 kernel's LDS ring) run on the layered path too
+  int kmax_ops = 0;
+  for (int i = 0; i < desc.n_ops; ++i)
+    if (desc.ops[i].kind == ZF_OP_NSC && desc.ops[i].knots > kmax_ops) kmax_ops = desc.ops[i].knots;
+  const bool layered = F.HP > zf::kMaxFusedWidth || kmax_ops > zf::kMaxFusedKnots;
   if (layered) F.HP = 32;  // the fused layouts below are then not built
   int x3K = 0;
   // the split-MFMA kernel runs hidden <= 128 padded to 128 (4 tiles)
@@ -631,7 +640,7 @@ int zf_flow_create(const zf_flow_desc* desc_in, const float* blob_host, int64_t 
   }
   if (x3 && zf::x3_lds_bytes(zf::x3_buf_tiles(desc, T, x3K), desc.dim + desc.cond_dim, NT, F.x3_par_bytes) <=
                 160 * 1024) {
-    zf::x3_pack(desc, nat, T, NT, F, P, x3s);
+    zf::x3_pack(desc, nat, T, NT, x3K, F, P, x3s);
     F.x3_ok = NT == 3 ? 1 : 2;
     h->x3_K = x3K;
     for (int i = 0; i < desc.n_ops; ++i)

@@ -378,7 +378,7 @@ int x3_buf_tiles(const zf_flow_desc& desc, int T, int K);
 size_t x3_lds_bytes(int TB, int D, int NT, int par_bytes);
 int x3_scheme();
 int x3_scheme_for(const zf_flow_desc& desc);
-void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, int Kp, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream);
 
 }  // namespace zf

@@ -15,6 +15,7 @@ namespace zf {
 int launch_x3_k8(const X3Launch& a, bool inverse);
 int launch_x3_k16(const X3Launch& a, bool inverse);
 int launch_x3_k32(const X3Launch& a, bool inverse);
+int launch_x3_k64(const X3Launch& a, bool inverse);
 
 namespace {
 
@@ -57,8 +58,7 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
     // a cancellation of 1e3-size products) bf16x3's mean error was 5x the
     // fp32 oracle's (scripts/diag_acts.py).
     if (op.act == ZF_ACT_SOFTPLUS && x3_scheme() == 3) return false;
-    if (K == 0) K = op.knots;
-    if (op.knots != K) return false;
+    if (op.knots > K) K = op.knots;  // a chain may mix knot counts: all run at the largest one's instantiation
   }
   // hidden <= 128 runs padded to 128 (the caller pads HP); any dim the
   // fp32 kernel takes (LDS is checked at create time)
@@ -73,13 +73,16 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
 // heights enter the sums as exact zeros (logit -2^40: squareplus = 0) and
 // their slope logits are 0 at the last real knot (the boundary derivative
 // 1) and NaN beyond, so the idx == K sliver still gives NaN (utils.py:
-// 224-230).  K = Kp - 1 is padded one size further: there the sliver bin
-// would be the instantiation's last, whose right slope is the boundary.
+// 224-230).  K = Kp - 1 has no NaN slope: the kernel starts the sliver at
+// knot K itself (rqs_bin_monotone's padlast, per coupling).  K in 33..64
+// runs at 64 (one wave per SIMD: 12 last-layer tiles and 191 spline
+// parameters per lane, x3_occupancy).
 int x3_padded_knots(int K) {
   if (K < 2) return 0;
-  if (K <= 8 && K != 7) return 8;
-  if (K <= 16 && K != 15) return 16;
-  if (K <= 32 && K != 31) return 32;
+  if (K <= 8) return 8;
+  if (K <= 16) return 16;
+  if (K <= 32) return 32;
+  if (K <= 64) return 64;
   return 0;
 }
 
@@ -123,7 +126,7 @@ int x3_pairs(const zf_flow_desc& desc) { return (desc.dim / 2 + 1) / 2; }
 // Pack the group streams (bf16 hi/mid/lo A fragments) of every NSC and the
 // row-permuted last-layer biases (into `packed` at F.ops[i].x3_blast, which
 // the caller allocated with x3_pairs * x3_last_tiles(K) * 32 floats).
-void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow& F, float* packed,
+void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, int Kp, DevFlow& F, float* packed,
              std::vector<uint16_t>& stream) {
   stream.clear();
   int prev = -1;
@@ -138,7 +141,7 @@ void x3_pack(const zf_flow_desc& desc, const float* nat, int T, int NT, DevFlow&
     if (op.kind != ZF_OP_NSC) continue;
     DevOp& d = F.ops[i];
     // K: the coupling's knots; Kp: the instantiation's (x3_padded_knots)
-    const int dt = desc.dim / 2, K = x3_padded_knots(op.knots), S = 3 * K - 1;
+    const int dt = desc.dim / 2, K = Kp, S = 3 * K - 1;  // every coupling at the flow's instantiation
     const int Kr = op.knots, Sr = 3 * Kr - 1;
     const bool one = dt == 1;
     const int TL = one ? x3_last_tiles_one(K) : x3_last_tiles(K), NP = x3_pairs(desc);
@@ -325,6 +328,7 @@ int launch_flow_x3(const X3Launch& a, bool inverse) {
   if (a.K == 8) return launch_x3_k8(a, inverse);
   if (a.K == 16) return launch_x3_k16(a, inverse);
   if (a.K == 32) return launch_x3_k32(a, inverse);
+  if (a.K == 64) return launch_x3_k64(a, inverse);
   return enotsup("split-MFMA kernel: knots not instantiated");
 }
 

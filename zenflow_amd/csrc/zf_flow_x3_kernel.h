@@ -491,7 +491,7 @@ __device__ __forceinline__ int first_pieces(const DevOp& op) {
 // of a chain of load -> wait -> branch -> load (each lgkmcnt(0) wait there
 // also drains the wave's outstanding LDS reads).
 struct X3Sc {
-  int kind, shift, nh, act, dt, dc, DC, KS0, G, tlast, nxt, npieces, npar, kw1, kw_last;
+  int kind, shift, nh, act, dt, dc, DC, KS0, G, tlast, nxt, npieces, npar, kw1, kw_last, kreal;
   long long x3, nbase, nbn, bn, w0_rel, b_rel, blast_rel, sb;
 };
 
@@ -504,6 +504,7 @@ __device__ __forceinline__ X3Sc x3_scalars(const DevOp& op) {
   c.G = op.x3_groups; c.tlast = op.x3_tlast; c.nxt = op.x3_next[d];
   c.npieces = op.x3_npieces[d]; c.npar = op.x3_npar[d];
   c.kw1 = op.x3_kw[1];
+  c.kreal = op.K;  // this coupling's knots (the kernel's K may be padded above them)
   c.kw_last = op.x3_kw[op.n_hidden & 15];
   c.x3 = op.x3; c.nbase = op.x3_nbase[d]; c.nbn = op.x3_nbn[d]; c.bn = op.bn;
   c.w0_rel = op.w[0] - op.bn; c.b_rel = op.b[0] - op.bn; c.blast_rel = op.x3_blast - op.bn;
@@ -655,11 +656,6 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   p.tbar += X3T_NOW() - tb0;
 #endif
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
-  floatx16 bt[NOUT];
-  if constexpr (HASB) {
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-  }
   const char* lb = p.cur + lane * 16;
   E s1[NT];
   splitk<NT, 1>(hb[Q], s1);
@@ -694,8 +690,10 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 #endif
   }
   if constexpr (HASB) {
+    // the layer end, acc * us + bias; each bias tile read as it is used, after
+    // the group's MFMAs (no 16 x NOUT registers held across them)
 #pragma unroll
-    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
+    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bias_acc(bias + o * 32, hh));
   }
 #if defined(ZF_X3_EXP) && ZF_X3_EXP == 3
   // experimental: each (k-step, tile) triple as [2 fragment reads][VALU x5]
@@ -1488,7 +1486,7 @@ template <int T, int K, bool PAIRS>
 #if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
 constexpr int x3_occupancy() { return T == 8 ? 1 : 2; }
 #else
-constexpr int x3_occupancy() { return T == 8 ? 1 : (PAIRS || K > 16) ? 2 : 3; }
+constexpr int x3_occupancy() { return (T == 8 || K > 32) ? 1 : (PAIRS || K > 16) ? 2 : 3; }
 #endif
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT, int ASET = 0>
@@ -1580,12 +1578,6 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   }
   int nsc_i = 0;  // NSCs entered, in execution order: parameter region nsc_i & 1
 
-  const KnotConsts kc(F->kreal);  // the couplings' knots (K may be padded above them)
-#ifdef ZF_X3_MARK
-  const bool klit = true;  // marker builds: count one x3_bin copy
-#else
-  const bool klit = F->kreal == K;  // x3_bin: the knot constants as literals
-#endif
   const int nq = op_end - op_begin;
   for (int q = 0; q < nq; ++q) {
     const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
@@ -1613,6 +1605,16 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       const float* par = reinterpret_cast<const float*>(par_lds + (nsc_i & 1) * PB);
       ++nsc_i;
       const int nh = opc.nh, act = opc.act, dt = opc.dt, kw_last = opc.kw_last;
+      // this coupling's knots: a chain may mix knot counts up to the kernel's K
+      // (x3_padded_knots); K - 1 real knots put the idx == K sliver at the
+      // padded knot (rqs_bin_monotone padlast)
+      const KnotConsts kc(opc.kreal);
+      const bool padlast = opc.kreal == K - 1;
+#ifdef ZF_X3_MARK
+      const bool klit = true;  // marker builds: count one x3_bin copy
+#else
+      const bool klit = opc.kreal == K;  // x3_bin: the knot constants as literals
+#endif
       // hidden biases are consecutive T x 32 blocks after Dense_0's (zf_flow.hip: b[l] = b[0] + l T 32)
       const long long b_rel = opc.b_rel + T * 32, blast_rel = opc.blast_rel;
       floatx16 hb[T];
@@ -1660,7 +1662,11 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       // f16x2 at hidden 128 (the slot schedule): zero-seeded accumulators and
       // one fma per value at the layer end (acc * us + bias) instead of a
       // bias * ius seed and an acc * us unscale (two multiplies per value)
-      constexpr bool kSeedScaled = NT == 2 && (ZF_X3_SEEDSCALED || !kPipe || OACT);
+      // (OACT too since round 5: a seeded bias sets the magnitude every MFMA
+      // accumulation rounds at; sigmoid / softplus fold C colsum(W) into it,
+      // 1e3-1e4 in the tiny-activation regime, where the zero-seeded sums of
+      // the small centred terms plus one finish fma round far less)
+      constexpr bool kSeedScaled = NT == 2 && (ZF_X3_SEEDSCALED || !kPipe);
       // the hidden layers of a dim-pair flow (d8, d16: PAIRS, 2 waves per
       // SIMD) and of hidden-256 flows (cfg5: T = 8, one wave per SIMD) take
       // the f16x2 slot schedule too: only the last layer, which re-reads its
@@ -1673,7 +1679,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #define ZF_X3_PAIRS_PIPE 1
 #endif
       constexpr bool kPipeH = kPipe || (ZF_X3_PAIRS_PIPE && (T == 4 || ZF_X3_WIDE_PIPE) && NT == 2 && !OACT);
-      constexpr bool kSeedScaledH = NT == 2 && (ZF_X3_SEEDSCALED || !kPipeH || OACT);
+      constexpr bool kSeedScaledH = NT == 2 && (ZF_X3_SEEDSCALED || !kPipeH);
       // Three waves share a SIMD at hidden 128: the one streaming weight
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
       // phases (layer 0, spline), so the matrix pipe idles less (+1.5% cfg2,
@@ -1856,9 +1862,14 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #define ZF_X3_BSEARCH 0
 #endif
           RqsBin bin;
-          if constexpr (ZF_X3_BSEARCH && !kSplitWH && (K == 8 || K == 16 || K == 32)) {
-            bin = klit ? x3_bin<!INV, K, OACT, true>(xv, P, kc) : x3_bin<!INV, K, OACT, false>(xv, P, kc);
-          } else {
+          bool binned = false;
+          if constexpr (ZF_X3_BSEARCH && !kSplitWH && (K == 8 || K == 16 || K == 32 || K == 64)) {
+            if (klit) {  // the halving search takes unpadded knots only
+              bin = x3_bin<!INV, K, OACT, true>(xv, P, kc);
+              binned = true;
+            }
+          }
+          if (!binned) {
             float w[K], hg[K];
             const float bc = kc.c * kc.rnorm;
             if constexpr (kSplitWH) {
@@ -1900,8 +1911,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
             float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
             for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
-            bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl,
-                                                         [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); });
+            bin = rqs_bin_monotone<!INV, K>(
+                xv, w, hg, sl, [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); }, padlast);
             X3M(13);
           }
           float yv;

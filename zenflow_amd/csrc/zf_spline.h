@@ -171,12 +171,13 @@ __device__ __forceinline__ RqsBin rqs_bin_regs_sl(float v, const float (&w)[K], 
 // NaN fill at idx == K (utils.py:224-230).
 template <bool FWD, int K, class TF>
 __device__ __forceinline__ RqsBin rqs_bin_monotone(float v, const float (&w)[K], const float (&h)[K],
-                                                   const float (&sl)[K - 1], const TF& sp) {
+                                                   const float (&sl)[K - 1], const TF& sp, bool padlast = false) {
   // knot 0 (at 0) latched up front: for v >= 0 it is the first knot <= v,
   // and for v < 0 (out of bounds: identity) or NaN the bin is unused
   float sxk = 0.f, syk = 0.f, sw = w[0], sh = h[0];
   float lo = 0.f, hi = (K > 1) ? sl[0] : 0.f;  // logits of dk, dk+1 at the current bin
   float xk = w[0], yk = h[0];
+  float xkm = xk, ykm = yk;  // knot K-1 (padlast)
   // branch-free latch (selects, not exec-masked moves)
 #pragma unroll
   for (int j = 1; j < K; ++j) {
@@ -187,12 +188,20 @@ __device__ __forceinline__ RqsBin rqs_bin_monotone(float v, const float (&w)[K],
     sh = c ? h[j] : sh;
     lo = c ? sl[j - 1] : lo;
     hi = c ? ((j + 1 < K) ? sl[j] : 0.f) : hi;
+    if (j == K - 1) { xkm = xk; ykm = yk; }
     xk = xk + w[j];
     yk = yk + h[j];
   }
   {
-    const float kk = FWD ? xk : yk;
-    if (kk <= v) { sxk = xk; syk = yk; sw = qnan(); sh = qnan(); lo = 0.f; hi = qnan(); }
+    // padlast: knot K-1 is the couplings' last real knot (the split-MFMA
+    // kernels run K-1 knots padded with one inert knot, x3_padded_knots), so
+    // the idx == K sliver starts there
+    const float kk = padlast ? (FWD ? xkm : ykm) : (FWD ? xk : yk);
+    if (kk <= v) {
+      sxk = padlast ? xkm : xk;
+      syk = padlast ? ykm : yk;
+      sw = qnan(); sh = qnan(); lo = 0.f; hi = qnan();
+    }
   }
   RqsBin b;
   b.xk = sxk;

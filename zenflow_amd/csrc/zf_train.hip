@@ -2329,7 +2329,9 @@ int dense_gemm(long long Mg, int M, int N, int K, const float* A, int lda, const
 int spline_rows(bool inverse, const float* s_in, float* s_out, const float* P, float* ld, int B, int D, int dt,
                 int K, int rot, hipStream_t st) {
   if (B <= 0) return ZF_OK;
-  if (dt < 1 || dt > kSplThreads || K < 1 || K > kMaxK) return enotsup("spline rows: transformed dims or knots out of range");
+  // the layered eval path takes up to 200 knots (the block's rows of 3K - 1
+  // parameters staged in LDS: 64 x 599 floats); training stays at kMaxK
+  if (dt < 1 || dt > kSplThreads || K < 1 || K > 200) return enotsup("spline rows: transformed dims or knots out of range");
   const int S = 3 * K - 1, rpb = kSplThreads / dt;
   const size_t lds = (size_t)kSplThreads * S * sizeof(float);
   if (inverse) {
