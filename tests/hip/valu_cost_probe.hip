@@ -12,9 +12,9 @@
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 
-enum { OP_FMA, OP_MUL, OP_EXP, OP_RCP, OP_SQRT, OP_MIX, OP_CVTPK, OP_MAX3, OP_CND, OP_PKFMA, OP_CVTF16, OP_CVTF16HI, OP_AND, OP_PKMUL, OP_LDEXP, OP_LOG, OP_MAX, OP_CNDS, OP_NONE };
+enum { OP_FMA, OP_MUL, OP_EXP, OP_RCP, OP_SQRT, OP_MIX, OP_CVTPK, OP_MAX3, OP_CND, OP_PKFMA, OP_CVTF16, OP_CVTF16HI, OP_AND, OP_PKMUL, OP_LDEXP, OP_LOG, OP_MAX, OP_CNDS, OP_MOV, OP_PKMOV, OP_PKADD, OP_CMPX, OP_EXP3FMA, OP_EXPMIX, OP_EXPCVT, OP_EXPRCP2FMA, OP_NONE };
 static const char* kNames[] = {"v_fma_f32", "v_mul_f32", "v_exp_f32", "v_rcp_f32", "v_sqrt_f32", "v_fma_mixlo_f16",
-                               "v_cvt_pk_f16_f32", "v_max3_f32", "v_cndmask_b32", "v_pk_fma_f32", "v_cvt_f32_f16", "v_cvt_f32_f16 sdwa", "v_and_b32", "v_pk_mul_f32", "v_ldexp_f32", "v_log_f32", "v_max_f32", "v_cndmask s[]", "none"};
+                               "v_cvt_pk_f16_f32", "v_max3_f32", "v_cndmask_b32", "v_pk_fma_f32", "v_cvt_f32_f16", "v_cvt_f32_f16 sdwa", "v_and_b32", "v_pk_mul_f32", "v_ldexp_f32", "v_log_f32", "v_max_f32", "v_cndmask s[]", "v_mov_b32", "v_pk_mov_b32", "v_pk_add_f32", "v_cmpx(all true)", "exp+3fma (/4)", "exp+mix (/2)", "exp+cvt_pk (/2)", "exp,rcp+2fma (/4)", "none"};
 
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 template <int OP>
@@ -36,6 +36,44 @@ __device__ __forceinline__ void op1(float& a, float b, float c) {
   if constexpr (OP == OP_LDEXP) asm volatile("v_ldexp_f32 %0, %0, %1" : "+v"(a) : "v"(b));
   if constexpr (OP == OP_LOG) asm volatile("v_log_f32 %0, %0" : "+v"(a));
   if constexpr (OP == OP_MAX) asm volatile("v_max_f32 %0, %1, %0" : "+v"(a) : "v"(b));
+  if constexpr (OP == OP_MOV) asm volatile("v_mov_b32 %0, %1" : "=v"(a) : "v"(b));
+  if constexpr (OP == OP_PKMOV) {
+    floatx2 x2 = {a, b};
+    asm volatile("v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]" : "+v"(x2));
+    a = x2[0];
+  }
+  if constexpr (OP == OP_PKADD) {
+    floatx2 x2 = {a, b};
+    asm volatile("v_pk_add_f32 %0, %0, %0" : "+v"(x2));
+    a = x2[0];
+  }
+  if constexpr (OP == OP_CMPX) asm volatile("v_cmpx_le_f32 vcc, %0, %1" : : "v"(b), "v"(a) : "vcc");  // b <= a: exec stays
+  if constexpr (OP == OP_PKFMA) {
+    floatx2 x2 = {a, b};
+    asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(x2));
+    a = x2[0];
+  }
+  if constexpr (OP == OP_EXP3FMA)
+  {
+    float t1, t2, t3;  // independent fmas beside the exp chain
+    asm volatile("v_exp_f32 %0, %0\n\tv_fma_f32 %1, %4, %4, %4\n\tv_fma_f32 %2, %4, %4, %4\n\tv_fma_f32 %3, %4, %4, %4"
+                 : "+v"(a), "=&v"(t1), "=&v"(t2), "=&v"(t3) : "v"(c));
+  }
+  if constexpr (OP == OP_EXPMIX)
+  {
+    float t1;
+    asm volatile("v_exp_f32 %0, %0\n\tv_fma_mixlo_f16 %1, %2, 1.0, -%2 op_sel_hi:[0,0,1]" : "+v"(a), "=&v"(t1) : "v"(c));
+  }
+  if constexpr (OP == OP_EXPCVT) {
+    float t1;
+    asm volatile("v_exp_f32 %0, %0\n\tv_cvt_pk_f16_f32 %1, %2, %2" : "+v"(a), "=&v"(t1) : "v"(c));
+  }
+  if constexpr (OP == OP_EXPRCP2FMA)
+  {
+    float t1, t2;
+    asm volatile("v_exp_f32 %0, %0\n\tv_fma_f32 %1, %3, %3, %3\n\tv_rcp_f32 %0, %0\n\tv_fma_f32 %2, %3, %3, %3"
+                 : "+v"(a), "=&v"(t1), "=&v"(t2) : "v"(c));
+  }
   if constexpr (OP == OP_CNDS) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(a) : "v"(b) : "s40", "s41");
 }
 
@@ -139,10 +177,19 @@ int main() {
   hipMalloc(&d, 256 * 16 * 8);
   h = (unsigned long long*)malloc(256 * 16 * 8);
   row<OP_FMA>(d, h);
-  row<OP_MUL>(d, h);
   row<OP_EXP>(d, h);
-  row<OP_RCP>(d, h);
-  row<OP_MIX>(d, h);
+  row<OP_EXP3FMA>(d, h);
+  row<OP_EXPRCP2FMA>(d, h);
+  row<OP_EXPMIX>(d, h);
+  row<OP_EXPCVT>(d, h);
+  row<OP_CND>(d, h);
   row<OP_CNDS>(d, h);
+  row<OP_MOV>(d, h);
+  row<OP_PKMOV>(d, h);
+  row<OP_PKADD>(d, h);
+  row<OP_PKFMA>(d, h);
+  row<OP_CMPX>(d, h);
+  row<OP_CVTPK>(d, h);
+  row<OP_AND>(d, h);
   return 0;
 }

@@ -966,7 +966,8 @@ __device__ __forceinline__ void x3_valu_slot_last(floatx16 (&hb)[T], floatx16 (&
   if constexpr (NEXT && m >= 8 && oq < NOUT && ((m - 8) % 6 == 0 || (m - 8) % 6 == 1)) {
     constexpr int r0 = (m - 8) % 6 == 0 ? 0 : 8;
 #pragma unroll
-    for (int r = r0; r < r0 + 8; r += 2) mx = fmaxf(mx, fmaxf(fabsf(acc[oq][r]), fabsf(acc[oq][r + 1])));
+    for (int r = r0; r < r0 + 8; r += 2)  // one v_max3 per two values (the compiler forms a max / max3 tree: 1.5x)
+      asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(acc[oq][r]), "v"(acc[oq][r + 1]));
   }
   if constexpr (NEXT) {
     constexpr int i0 = m - 9, i1 = m - 10, i2 = m - 11, i3 = m - 12;
@@ -1521,17 +1522,31 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   const long long row = ((long long)blockIdx.x * NW + wave) * kTile + s;
   const bool valid = row < N;
 
-  load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
-  for (int j = hh; j < C; j += 2) xs[(D + j) * 32 + s] = valid ? cin[row * C + j] : 0.f;
-  float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
-  int rot = 0;
-  wave_lds_sync();
-
   X3Pipe pipe;
   pipe.cur = lds;
   pipe.nxt = lds + kBuf;
   pipe.g = 0;
   pipe.wave = wave;
+  {  // group 0 and the small parameters of the first NSC in execution order go
+     // out before the state loads, so the block waits for one memory latency,
+     // not two in a row
+    int first = -1;
+    const int nq = op_end - op_begin;
+    for (int q = 0; q < nq; ++q) {
+      const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
+      if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
+    }
+    if (first >= 0) {
+      const DevOp& fo = F->ops[first];
+      x3_dma(x3 + fo.x3, pipe.cur, first_pieces<NT, T>(fo), wave, lane);
+      x3_dma(reinterpret_cast<const char*>(blob + fo.bn), par_lds, fo.x3_par_pieces, wave, lane);
+    }
+  }
+  load_state(xs, xin, row, valid, D, s, hh, F, seed, INV ? gen : 0);
+  for (int j = hh; j < C; j += 2) xs[(D + j) * 32 + s] = valid ? cin[row * C + j] : 0.f;
+  float ld = (ld_in != nullptr && valid) ? ld_in[row] : 0.f;
+  int rot = 0;
+  wave_lds_sync();
 #ifdef ZF_X3_TRACE
   // slots: 0 start->first NSC, 1 layer 0, 2 hidden layers, 3 hidden->last
   // transition, 4 last layer, 5 spline, 6 epilogue, 7 barrier waits (inside
@@ -1560,19 +1575,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   pipe.par_src = nullptr;
   pipe.par_dst = nullptr;
   pipe.par_pieces = 0;
-  {  // group 0 and the small parameters of the first NSC in execution order go out now
-    int first = -1;
-    const int nq = op_end - op_begin;
-    for (int q = 0; q < nq; ++q) {
-      const int oi = INV ? (op_end - 1 - q) : (op_begin + q);
-      if (F->ops[oi].kind == ZF_OP_NSC) { first = oi; break; }
-    }
-    if (first >= 0) {
-      const DevOp& fo = F->ops[first];
-      x3_dma(x3 + fo.x3, pipe.cur, first_pieces<NT, T>(fo), wave, lane);
-      x3_dma(reinterpret_cast<const char*>(blob + fo.bn), par_lds, fo.x3_par_pieces, wave, lane);
-    }
-    // its layer 0 reads the parameters before any group step's wait
+  {  // the first NSC's layer 0 reads the parameters before any group step's wait
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -1911,8 +1914,13 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
             float sl[K - 1];  // raw slope logits; the bin's two get squareplus'd
 #pragma unroll
             for (int j = 0; j < K - 1; ++j) sl[j] = P[2 * K + j];
-            bin = rqs_bin_monotone<!INV, K>(
-                xv, w, hg, sl, [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); }, padlast);
+#ifndef ZF_X3_EXECBIN
+#define ZF_X3_EXECBIN 1
+#endif
+            // the latch as exec-masked moves (rqs_bin_exec): -15% of the spline phase's VALU issue
+            const auto spf = [](float v) { return v == 0.f ? 1.f : x3_squareplus_t<OACT>(v); };
+            if constexpr (ZF_X3_EXECBIN && K % 8 == 0) bin = rqs_bin_exec<!INV, K>(xv, w, hg, sl, spf, padlast);
+            else bin = rqs_bin_monotone<!INV, K>(xv, w, hg, sl, spf, padlast);
             X3M(13);
           }
           float yv;

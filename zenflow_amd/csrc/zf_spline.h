@@ -215,6 +215,118 @@ __device__ __forceinline__ RqsBin rqs_bin_monotone(float v, const float (&w)[K],
   return b;
 }
 
+// rqs_bin_monotone's latch with exec-masked moves instead of selects
+// (split-MFMA kernels, monotone knots only).  The knots grow along j, so the
+// lanes whose knot j is <= v are a subset of those whose knot j-1 is: each
+// knot's v_cmpx narrows exec to them and the latch is plain v_mov / v_add
+// under that exec (8 full-rate VALU per knot against a compare, six
+// two-pass v_cndmask_b32_e64 and two adds).  The same adds in the same
+// order as rqs_bin_monotone's running sums (knot j = knot j-1 + w[j-1]),
+// so the latched values are bit-identical.  Eight knots per asm statement;
+// the narrowed exec is carried between statements in an SGPR pair.  The
+// latched values are early-clobber: an input equal in value to one of them
+// (a zero slope logit and the zero lo seed) must not share its register.
+#ifndef ZF_CMPX_NOP
+#define ZF_CMPX_NOP 0
+#endif
+#if ZF_CMPX_NOP
+#define ZF_CMPX_PAD "s_nop 4\n\t"
+#else
+#define ZF_CMPX_PAD ""
+#endif
+#define ZF_KNOT_F(i)                                                                                   \
+  "v_add_f32 %[t], %[sx], %[sw]\n\tv_cmpx_le_f32 vcc, %[t], %[v]\n\t" ZF_CMPX_PAD "v_mov_b32 %[sx], %[t]\n\t"       \
+  "v_add_f32 %[sy], %[sy], %[sh]\n\tv_mov_b32 %[sw], %[w" #i "]\n\tv_mov_b32 %[sh], %[h" #i "]\n\t" \
+  "v_mov_b32 %[lo], %[hi]\n\tv_mov_b32 %[hi], %[s" #i "]\n\t"
+#define ZF_KNOT_I(i)                                                                                   \
+  "v_add_f32 %[t], %[sy], %[sh]\n\tv_cmpx_le_f32 vcc, %[t], %[v]\n\t" ZF_CMPX_PAD "v_mov_b32 %[sy], %[t]\n\t"       \
+  "v_add_f32 %[sx], %[sx], %[sw]\n\tv_mov_b32 %[sw], %[w" #i "]\n\tv_mov_b32 %[sh], %[h" #i "]\n\t" \
+  "v_mov_b32 %[lo], %[hi]\n\tv_mov_b32 %[hi], %[s" #i "]\n\t"
+#define ZF_KNOT_OPS(i) [w##i] "v"(w[i]), [h##i] "v"(h[i]), [s##i] "v"(s[i])
+#define ZF_KNOT_OUTS                                                                                 \
+  [sx] "+&v"(sx), [sy] "+&v"(sy), [sw] "+&v"(sw), [sh] "+&v"(sh), [lo] "+&v"(lo), [hi] "+&v"(hi), [m] "+s"(m), \
+      [t] "=&v"(t), [sv] "=&s"(sv)
+
+template <bool FWD, int N>
+__device__ __forceinline__ void knot_chunk(unsigned long long& m, float v, float& sx, float& sy, float& sw, float& sh,
+                                           float& lo, float& hi, const float* w, const float* h, const float* s) {
+  static_assert(N == 7 || N == 8, "knot chunks of 7 or 8");
+  float t;
+  unsigned long long sv;
+#define ZF_CHUNK(KN, ...)                                                                                        \
+  asm("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\t" KN(0) KN(1) KN(2) KN(3) KN(4) KN(5) KN(6) __VA_ARGS__ \
+      "s_mov_b64 %[m], exec\n\ts_mov_b64 exec, %[sv]"                                                           \
+      : ZF_KNOT_OUTS                                                                                             \
+      : [v] "v"(v), ZF_KNOT_OPS(0), ZF_KNOT_OPS(1), ZF_KNOT_OPS(2), ZF_KNOT_OPS(3), ZF_KNOT_OPS(4), ZF_KNOT_OPS(5), \
+        ZF_KNOT_OPS(6)ZF_CHUNK_LAST                                                                             \
+      : "vcc")
+  if constexpr (N == 8) {
+#define ZF_CHUNK_LAST , ZF_KNOT_OPS(7)
+    if constexpr (FWD) ZF_CHUNK(ZF_KNOT_F, ZF_KNOT_F(7));
+    else ZF_CHUNK(ZF_KNOT_I, ZF_KNOT_I(7));
+#undef ZF_CHUNK_LAST
+  } else {
+#define ZF_CHUNK_LAST
+    if constexpr (FWD) ZF_CHUNK(ZF_KNOT_F, );
+    else ZF_CHUNK(ZF_KNOT_I, );
+#undef ZF_CHUNK_LAST
+  }
+#undef ZF_CHUNK
+}
+
+template <bool FWD, int K, class TF>
+__device__ __forceinline__ RqsBin rqs_bin_exec(float v, const float (&w)[K], const float (&h)[K],
+                                               const float (&sl)[K - 1], const TF& sp, bool padlast) {
+  static_assert(K % 8 == 0, "knot chunks of 8");
+  float sx = 0.f, sy = 0.f, sw = w[0], sh = h[0], lo = 0.f, hi = sl[0];
+  float s2[K];  // slope logit j for knot j's upper neighbour; 0 past the last inner knot
+#pragma unroll
+  for (int j = 0; j < K - 1; ++j) s2[j] = sl[j];
+  s2[K - 1] = 0.f;
+  unsigned long long m = __builtin_amdgcn_read_exec();
+  knot_chunk<FWD, 7>(m, v, sx, sy, sw, sh, lo, hi, w + 1, h + 1, s2 + 1);
+#pragma unroll
+  for (int c = 8; c < K; c += 8) knot_chunk<FWD, 8>(m, v, sx, sy, sw, sh, lo, hi, w + c, h + c, s2 + c);
+  // the idx == K sliver: past knot K (or past the last real knot K-1, padlast)
+  {
+    float t;
+    unsigned long long sv;
+    const float nan = qnan();
+    if (padlast) {
+      asm("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\t"
+          "v_mov_b32 %[sw], %[nan]\n\tv_mov_b32 %[sh], %[nan]\n\tv_mov_b32 %[lo], 0\n\tv_mov_b32 %[hi], %[nan]\n\t"
+          "s_mov_b64 exec, %[sv]"
+          : [sw] "+&v"(sw), [sh] "+&v"(sh), [lo] "+&v"(lo), [hi] "+&v"(hi), [sv] "=&s"(sv)
+          : [m] "s"(m), [nan] "v"(nan));
+      (void)t;
+    } else {
+      asm("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, %[m]\n\t"
+          "v_add_f32 %[t], %[a], %[da]\n\tv_cmpx_le_f32 vcc, %[t], %[v]\n\t" ZF_CMPX_PAD "v_mov_b32 %[a], %[t]\n\t"
+          "v_add_f32 %[b], %[b], %[db]\n\t"
+          "v_mov_b32 %[sw], %[nan]\n\tv_mov_b32 %[sh], %[nan]\n\tv_mov_b32 %[lo], 0\n\tv_mov_b32 %[hi], %[nan]\n\t"
+          "s_mov_b64 exec, %[sv]"
+          : [a] "+&v"(FWD ? sx : sy), [b] "+&v"(FWD ? sy : sx), [sw] "+&v"(sw), [sh] "+&v"(sh), [lo] "+&v"(lo),
+            [hi] "+&v"(hi), [t] "=&v"(t), [sv] "=&s"(sv)
+          : [m] "s"(m), [nan] "v"(nan), [v] "v"(v), [da] "v"(FWD ? sw : sh), [db] "v"(FWD ? sh : sw)
+          : "vcc");
+    }
+  }
+  RqsBin b;
+  b.xk = sx;
+  b.yk = sy;
+  b.w = sw;
+  b.h = sh;
+  b.dk = sp(lo);
+  b.dkp1 = sp(hi);
+  b.sk = b.h / b.w;
+  b.oob = (v < 0.f) || (v >= 1.f);
+  return b;
+}
+#undef ZF_KNOT_F
+#undef ZF_KNOT_I
+#undef ZF_KNOT_OPS
+#undef ZF_KNOT_OUTS
+
 // utils.py:121-139 — forward value and per-dim log|dy/dx|.
 __device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
   const float zr = (x - b.xk) / b.w;               // :122
