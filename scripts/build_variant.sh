@@ -1,14 +1,21 @@
 #!/bin/bash
-# Tuning: a library variant that differs from the in-tree build only in the
-# K = 16 split-MFMA translation unit, compiled with extra flags:
-#   scripts/build_variant.sh NAME [-DFLAG=V ...]  ->  tune/libNAME.so
+# Tuning: a library variant that differs from the in-tree build only in some
+# split-MFMA translation units (TUS, default the K = 16 one), compiled with
+# extra flags:
+#   [TUS="k16 k16_act2"] scripts/build_variant.sh NAME [-DFLAG=V ...]  ->  tune/libNAME.so
 # (links the other objects of the last default build, build/obj/*.o)
 set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift
 mkdir -p tune
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-result -I/opt/rocm/include -Iinclude -fno-slp-vectorize"
-/opt/rocm/bin/hipcc $FLAGS "$@" -c -o tune/k16_$NAME.o zenflow_amd/csrc/zf_flow_x3_k16.hip
-OBJS=$(ls build/obj/*.o | grep -v zf_flow_x3_k16.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tune/lib$NAME.so $OBJS tune/k16_$NAME.o -ldl
+OBJS=$(ls build/obj/*.o)
+NEW=""
+for tu in ${TUS:-k16}; do
+  /opt/rocm/bin/hipcc $FLAGS "$@" -c -o tune/${tu}_$NAME.o zenflow_amd/csrc/zf_flow_x3_$tu.hip &
+  OBJS=$(echo "$OBJS" | grep -v "/zf_flow_x3_$tu.o")
+  NEW="$NEW tune/${tu}_$NAME.o"
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tune/lib$NAME.so $OBJS $NEW -ldl
 echo tune/lib$NAME.so
