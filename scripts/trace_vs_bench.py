@@ -18,12 +18,12 @@ from pathlib import Path
 PEAK = 2516.6 / 3  # TFLOP/s, fp16 dense / 3
 # config -> (template args of flow_kernel_x3, alg flops per sample)
 KERNELS = {
-    "cfg2": ("<2, 16, 4, false, false, false, false>", 229376),
-    "cfg3": ("<2, 16, 4, false, false, true, false>", 229376),
-    "cfg3s": ("<2, 16, 4, false, false, true, false>", 229376),
-    "cfg4": ("<2, 16, 4, false, true, false, false>", 91136),
-    "cfg5": ("<2, 32, 8, true, false, false, false>", 4194304),
-    "d8": ("<2, 16, 4, true, false, false, false>", 2 * 8 * (4 * 128 + 128 * 128 + 128 * 4 * 47)),
+    "cfg2": ("<2, 16, 4, false, false, false, false, 0>", 229376),
+    "cfg3": ("<2, 16, 4, false, false, true, false, 0>", 229376),
+    "cfg3s": ("<2, 16, 4, false, false, true, false, 0>", 229376),
+    "cfg4": ("<2, 16, 4, false, true, false, false, 0>", 91136),
+    "cfg5": ("<2, 32, 8, true, false, false, false, 0>", 4194304),
+    "d8": ("<2, 16, 4, true, false, false, false, 0>", 2 * 8 * (4 * 128 + 128 * 128 + 128 * 4 * 47)),
 }
 ROWS = 1 << 20
 

@@ -639,7 +639,7 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 // (Q+1, 0) for the next group — so the bf16 split and the deferred swish sit
 // in the MFMA issue gaps of the same wave (cross-wave they would not overlap:
 // tests/hip/coexec_probe.hip modes 2 and 6).
-template <int NT, int T, int NOUT, int Q, bool HASB, bool OACT>
+template <int NT, int T, int NOUT, int Q, bool HASB, bool OACT, int AS = 0>
 __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                              floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
                                              int hh, typename XT<NT>::E (&cs)[NT], float isc, float us,
@@ -675,7 +675,9 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
   }
   if constexpr (Q + 1 < T) {
 #if ZF_X3_ABL != 2  // tuning ablation 2: no swish inside the group steps (wrong results)
-    if constexpr (!OACT) x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
+    // OACT with a narrowed activation set (AS, f16x2): tile Q+1's activation
+    // here too, beside this group's MFMAs (not serially at the layer end)
+    if constexpr (!OACT || (NT == 2 && AS != 0)) x3_act_tile<NT, OACT, AS>(hb[Q + 1], isc, act);
 #endif
     splitk<NT, 0>(hb[Q + 1], cs);
   }
@@ -695,84 +697,12 @@ __device__ __forceinline__ void x3_step_pipe(const char* __restrict__ x3, X3Pipe
 #pragma unroll
     for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bias_acc(bias + o * 32, hh));
   }
-#if defined(ZF_X3_EXP) && ZF_X3_EXP == 3
-  // experimental: each (k-step, tile) triple as [2 fragment reads][VALU x5]
-  // [MFMA][VALU x3][MFMA][VALU x3][MFMA], so the step's VALU issues between
-  // the dependent MFMAs of a triple instead of after it
-  {
-#pragma unroll
-    for (int i = 0; i < 2 * NOUT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-#pragma unroll
-      for (int m = 0; m < XT<NT>::kProd; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (m + 1 < XT<NT>::kProd) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      }
-    }
-  }
-#endif
   char* const t = p.cur;
   p.cur = p.nxt;
   p.nxt = t;
   p.g += 1;
 }
 
-#ifdef ZF_X3_EXP
-// Experimental (tuning builds): the group's A fragments all read from LDS at
-// the step's start (2 x NOUT x NT ds_read_b128, counted waits), so the MFMAs
-// do not wait on an LDS round trip per (k-step, tile); ZF_X3_EXP >= 2 also
-// interleaves the step's VALU evenly between its MFMAs.
-template <int NT, int T, int NOUT, int Q, bool HASB, bool OACT>
-__device__ __forceinline__ void x3_step_up(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
-                                           floatx16 (&acc)[NOUT], int lane, const float* __restrict__ bias,
-                                           int hh, typename XT<NT>::E (&cs)[NT], float isc, float us, int act) {
-  using E = typename XT<NT>::E;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  x3_issue_next<NT, T>(x3, p, p.nxt, lane);
-  floatx16 bt[NOUT];
-  if constexpr (HASB) {
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) bt[o] = bias_acc(bias + o * 32, hh);
-  }
-  const char* lb = p.cur + lane * 16;
-  E fa[2][NOUT][NT];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) load_frag<NT>(lb + (((s2 * NOUT + o) * NT) << 10), fa[s2][o]);
-  E s1[NT];
-  splitk<NT, 1>(hb[Q], s1);
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) acc[o] = mfma_split<NT>(fa[0][o], cs, acc[o]);
-  if constexpr (Q + 1 < T) {
-    if constexpr (!OACT) x3_act_tile<NT, OACT>(hb[Q + 1], isc, act);
-    splitk<NT, 0>(hb[Q + 1], cs);
-  }
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) acc[o] = mfma_split<NT>(fa[1][o], s1, acc[o]);
-  if constexpr (HASB) {
-#pragma unroll
-    for (int o = 0; o < NOUT; ++o) acc[o] = x3_finish<NT>(acc[o], us, bt[o]);
-  }
-#if ZF_X3_EXP >= 2
-  {
-    constexpr int kM = 2 * NOUT * XT<NT>::kProd;
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * NOUT * NT, 0);
-#pragma unroll
-    for (int i = 0; i < kM; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-    }
-  }
-#endif
-  char* const t = p.cur;
-  p.cur = p.nxt;
-  p.nxt = t;
-  p.g += 1;
-}
-#endif
 
 // One product term of a (k-step, tile) triple: j = 0: lo*hi, 1: hi*lo, 2: hi*hi
 // (f16x2, small terms first as mfma_split).
@@ -1191,16 +1121,11 @@ __device__ __forceinline__ void x3_layer_pre(const char* __restrict__ x3, X3Pipe
 }
 
 // A pipelined layer: hb[0] already swished, cs = split of (0, 0).
-template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0>
+template <int NT, int T, int NOUT, bool HASB, bool OACT, int Q = 0, int AS = 0>
 __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pipe& p, floatx16 (&hb)[T],
                                               floatx16 (&acc)[NOUT], int lane, const float* bias_last, int hh,
                                               typename XT<NT>::E (&cs)[NT], float isc, float us, int act,
                                               halfx8 (&fused_s1)[2]) {
-#if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
-#define X3_STEP x3_step_up
-#else
-#define X3_STEP x3_step_pipe
-#endif
 #ifndef ZF_X3_FUSED
 #define ZF_X3_FUSED 0
 #endif
@@ -1226,12 +1151,12 @@ __device__ __forceinline__ void x3_layer_pipe(const char* __restrict__ x3, X3Pip
     return;
   }
   if constexpr (Q + 1 < T) {
-    X3_STEP<NT, T, NOUT, Q, false, OACT>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
-    x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act, fused_s1);
+    x3_step_pipe<NT, T, NOUT, Q, false, OACT, AS>(x3, p, hb, acc, lane, nullptr, hh, cs, isc, us, act);
+    x3_layer_pipe<NT, T, NOUT, HASB, OACT, Q + 1, AS>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act,
+                                                      fused_s1);
   } else {
-    X3_STEP<NT, T, NOUT, Q, HASB, OACT>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
+    x3_step_pipe<NT, T, NOUT, Q, HASB, OACT, AS>(x3, p, hb, acc, lane, bias_last, hh, cs, isc, us, act);
   }
-#undef X3_STEP
 }
 
 // A layer of the early-scale path (f16x2 swish, hidden 128): steps 0..T-2 as
@@ -1484,11 +1409,7 @@ __device__ __forceinline__ RqsBin x3_bin(float v, const float (&P)[NPV], const K
 // all tiles before the layer's groups instead of tile by tile inside them
 // (a switch inside the pipelined steps spilled 110-130 VGPRs at 3 waves).
 template <int T, int K, bool PAIRS>
-#if defined(ZF_X3_EXP) && ZF_X3_EXP < 3
-constexpr int x3_occupancy() { return T == 8 ? 1 : 2; }
-#else
 constexpr int x3_occupancy() { return (T == 8 || K > 32) ? 1 : (PAIRS || K > 16) ? 2 : 3; }
-#endif
 
 template <int NT, int K, int T, bool PAIRS, bool ONE, bool INV, bool OACT, int ASET = 0>
 __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void flow_kernel_x3(
@@ -1682,6 +1603,13 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #define ZF_X3_PAIRS_PIPE 1
 #endif
       constexpr bool kPipeH = kPipe || (ZF_X3_PAIRS_PIPE && (T == 4 || ZF_X3_WIDE_PIPE) && NT == 2 && !OACT);
+      // OACT with a narrowed activation set: the layer input's tiles 1..T-1
+      // activated inside the group steps (x3_step_pipe AS), like the swish
+#ifndef ZF_X3_ACTIN
+#define ZF_X3_ACTIN 1
+#endif
+      // (the centred set only: the five-way plain set spills 40 VGPRs that way, -13% on relu)
+      constexpr bool kActIn = ZF_X3_ACTIN && NT == 2 && ASET == 2 && kPipeH;
       constexpr bool kSeedScaledH = NT == 2 && (ZF_X3_SEEDSCALED || !kPipeH);
       // Three waves share a SIMD at hidden 128: the one streaming weight
       // groups (MFMAs) wins issue arbitration over one in its VALU-only
@@ -1719,7 +1647,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           // OACT: every tile here, outside the MFMA stream (the switch there
           // would cost a third of the waves)
 #pragma unroll
-          for (int o = 0; o < (OACT ? T : 1); ++o) x3_act_tile<NT, OACT, ASET>(hb[o], isc, act);
+          for (int o = 0; o < (OACT && !kActIn ? T : 1); ++o) x3_act_tile<NT, OACT, ASET>(hb[o], isc, act);
         }
         const float* bl_l = par + b_rel + (l - 1) * (T * 32);
 #pragma unroll
@@ -1731,7 +1659,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
           halfx8 fs1[2];  // ZF_X3_FUSED: the k-step 1 terms carried between group steps
-          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaledH, OACT>(x3, pipe, hb, acc, lane, bh, hh, cs, isc, us,
+          x3_layer_pipe<NT, T, T, NT == 2 && !kSeedScaledH, OACT, 0, kActIn ? ASET : 0>(x3, pipe, hb, acc, lane, bh, hh,
+                                                                                     cs, isc, us,
                                                                  act, fs1);
         } else {
           x3_layer<NT, T, T, true, OACT>(x3, pipe, hb, acc, lane, bh, hh, isc, us, act);
@@ -1771,7 +1700,7 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         // PAIRS: the input is read once per dim pair, so swish it whole here
 #pragma unroll
         for (int o = 0; o < T; ++o)
-          if (o == 0 || !kLastSW || OACT) x3_act_tile<NT, OACT, ASET>(hb[o], lisc, act);
+          if (o == 0 || !kLastSW || (OACT && !(kActIn && kPipe))) x3_act_tile<NT, OACT, ASET>(hb[o], lisc, act);
       }
 #ifndef ZF_X3_PRESPLIT
 #define ZF_X3_PRESPLIT 1
@@ -1809,7 +1738,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           typename XT<NT>::E cs[NT];
           splitk<NT, 0>(hb[0], cs);
           halfx8 fs1[2];
-          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc, lus, act, fs1);
+          x3_layer_pipe<NT, T, TL, !kSeedScaled, OACT, 0, kActIn ? ASET : 0>(x3, pipe, hb, pa, lane, bl, hh, cs, lisc,
+                                                                             lus, act, fs1);
         } else {
           x3_layer<NT, T, TL, kLastSW, OACT>(x3, pipe, hb, pa, lane, (kSeed || kSeedScaled) ? nullptr : bl, hh,
                                              lisc, lus, act);
