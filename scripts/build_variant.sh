@@ -12,8 +12,10 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wn
 OBJS=$(ls build/obj/*.o)
 NEW=""
 for tu in ${TUS:-k16}; do
-  /opt/rocm/bin/hipcc $FLAGS "$@" -c -o tune/${tu}_$NAME.o zenflow_amd/csrc/zf_flow_x3_$tu.hip &
-  OBJS=$(echo "$OBJS" | grep -v "/zf_flow_x3_$tu.o")
+  # a split-MFMA unit by its suffix (k16, k16_act2) or any unit by its name (zf_rqs)
+  base=zf_flow_x3_$tu; [ -f zenflow_amd/csrc/$tu.hip ] && base=$tu
+  /opt/rocm/bin/hipcc $FLAGS "$@" -c -o tune/${tu}_$NAME.o zenflow_amd/csrc/$base.hip &
+  OBJS=$(echo "$OBJS" | grep -v "/$base.o")
   NEW="$NEW tune/${tu}_$NAME.o"
 done
 wait

@@ -55,6 +55,9 @@ CONFIGS = {
     "k64c1": dict(D=3, C=1, K=64, layers=(128, 128), latent="beta"),
     "k100": dict(D=4, C=0, K=100, layers=(128, 128), latent="normal"),
     "kmix": dict(D=4, C=0, K=(16, 8, 31, 12), layers=(128, 128), latent="normal"),
+    # a 1-knot coupling inside a mixed chain keeps the flow on the
+    # fp32 kernel (as a flow of 1-knot couplings is)
+    "kmix1": dict(D=4, C=0, K=(16, 1, 8, 12), layers=(128, 128), latent="normal"),
     # the ends of the knot range: two knots (padded to 8), 63 (one padded knot
     # on the K = 64 instantiation), 200 (the layered path's cap)
     "k2": dict(D=2, C=0, K=2, layers=(64, 64), latent="normal"),

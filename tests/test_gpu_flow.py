@@ -107,7 +107,7 @@ def test_inverse_parity(name):
     assert_allclose(x[both], ref[both], rtol=REL, atol=REL * np.abs(ref[both]).max())
 
 
-KNOT_SHAPES = ["k7", "k31", "k40", "k64", "k64c1", "kmix", "k100", "k2", "k63", "k200"]
+KNOT_SHAPES = ["k7", "k31", "k40", "k64", "k64c1", "kmix", "kmix1", "k100", "k2", "k63", "k200"]
 
 
 @pytest.mark.parametrize("name", KNOT_SHAPES)
@@ -120,7 +120,7 @@ def test_knot_counts(name):
     log_prob at N in {1, 1000, 4096}, the inverse, and forward(inverse(z)) = z."""
     case = make_case(name, N=8, seed=50)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == ("layered" if name in ("k100", "k200") else "f16x2")
+    assert bf.program.kernel_variant == {"k100": "layered", "k200": "layered", "kmix1": "fp32"}.get(name, "f16x2")
     for N in (1, 1000, 4096):
         case = make_case(name, N=N, seed=51 + N)
         check_lp(gpu_log_prob(case), case, f"{name}/N={N}")

@@ -380,6 +380,44 @@ def test_setup_reads_declared_param():
         Lone().n
 
 
+def test_setup_derived_values_follow_each_apply():
+    """values setup() derives from param values (``self.w2 =
+    self.w * 2``, ``self.bs = float(self.b.sum())``) follow the variables of
+    each apply call, as flax re-runs setup per bind — on a child and on the
+    top-level module — while a submodule that setup() creates again with the
+    same configuration keeps its instance (and with it its program cache)."""
+
+    class Child(zf.Module):
+        def setup(self):
+            self.w = self.param("w", lambda rng, shape: np.arange(shape[0], dtype=np.float32), (3,))
+            self.w2 = self.w * 2
+
+        def __call__(self, x):
+            return np.asarray(x, np.float32) * self.w2
+
+    class Top(zf.Module):
+        def setup(self):
+            self.child = Child()
+            self.flow = zf.Flow(bi.rolling_spline_coupling(2, knots=4, layers=(8,)))
+            self.b = self.param("b", lambda rng, shape: np.ones(shape, np.float32), (3,))
+            self.bs = float(self.b.sum())
+
+        def __call__(self, x):
+            return self.child(x) + self.bs
+
+    m = Top()
+    x = np.ones((2, 3), np.float32)
+    v1 = m.init(PRNGKey(0), x)
+    v2 = {"params": {"b": np.full(3, 5.0, np.float32), "child": {"w": np.full(3, 3.0, np.float32)}}}
+    np.testing.assert_allclose(m.apply(v1, x), x * np.arange(3) * 2 + 3.0)
+    child, flow = m.child, m.flow
+    flow.__dict__["_programs"] = {"marker": 1}
+    flow.latent._dim = 2  # lazily set state, as after a log_prob call
+    np.testing.assert_allclose(m.apply(v2, x), x * 6.0 + 15.0)  # w2 and bs of v2
+    np.testing.assert_allclose(m.apply(v1, x), x * np.arange(3) * 2 + 3.0)
+    assert m.child is child and m.flow is flow and flow.__dict__["_programs"] == {"marker": 1}
+
+
 def test_select_device_rules():
     """One rank per GPU: LOCAL_RANK picks the device; a rank masked down to
     one visible device uses it; ZF_DEVICE overrides (with a warning in a

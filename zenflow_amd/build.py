@@ -69,12 +69,20 @@ def build(force: bool = False, verbose: bool = True, out: Path = LIB, extra=()) 
     objdir.mkdir(parents=True, exist_ok=True)
     compile_flags = [f for f in FLAGS if f != "-shared"] + list(extra)
 
+    hdr = hashlib.sha256(b"".join((CSRC / f).read_bytes() for f in HEADERS) + (INCLUDE / "zenflow_amd.h").read_bytes())
+
     def _compile(src: str) -> Path:
         obj = objdir / (Path(src).stem + ".o")
         cmd = [HIPCC, *compile_flags, *_src_flags(src), "-c", "-o", str(obj), str(CSRC / src)]
+        # per-object stamp (source, every header, the command): unchanged units are not rebuilt
+        key = hashlib.sha256(hdr.digest() + (CSRC / src).read_bytes() + " ".join(cmd).encode()).hexdigest()
+        ostamp = obj.with_suffix(".o.sha256")
+        if not force and obj.exists() and ostamp.exists() and ostamp.read_text() == key:
+            return obj
         if verbose:
             print("[zenflow_amd.build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        ostamp.write_text(key)
         return obj
 
     # one hipcc per translation unit, in parallel (the kernels dominate build time)

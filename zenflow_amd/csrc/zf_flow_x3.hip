@@ -56,9 +56,14 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
     // runs uncentred and softplus stays on the fp32 kernel: in the
     // tiny-activation regime (deviations from log 2 under 1e4-scale weights,
     // a cancellation of 1e3-size products) bf16x3's mean error was 5x the
-    // fp32 oracle's (scripts/diag_acts.py).
+    // fp32 oracle's (profiles/r03_diag_acts.jsonl; held by
+    // tests/test_gpu_flow.py::test_split_scaling_extremes_other_acts).
     if (op.act == ZF_ACT_SOFTPLUS && x3_scheme() == 3) return false;
-    if (op.knots > K) K = op.knots;  // a chain may mix knot counts: all run at the largest one's instantiation
+    // a chain may mix knot counts: all run at the largest one's
+    // instantiation; a 1-knot coupling anywhere keeps the flow off it, as a
+    // flow of 1-knot couplings is (that case is not pinned)
+    if (op.knots < 2) return false;
+    if (op.knots > K) K = op.knots;
   }
   // hidden <= 128 runs padded to 128 (the caller pads HP); any dim the
   // fp32 kernel takes (LDS is checked at create time)

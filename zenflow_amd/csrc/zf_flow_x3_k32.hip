@@ -12,3 +12,10 @@ int launch_x3_k32(const X3Launch& a, bool inverse) {
 }
 
 }  // namespace zf
+
+#ifdef ZF_X3_TRACE
+// tuning build only: install the per-wave phase-trace buffer of the K = 32 kernels
+extern "C" int zf_x3_trace_set_k32(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(zf::x3_trace_buf), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif

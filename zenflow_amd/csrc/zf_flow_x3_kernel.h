@@ -847,7 +847,10 @@ __device__ __forceinline__ void x3_step_slots(const char* __restrict__ x3, X3Pip
 // MFMA sums are the same bits as with the exact scale unless the bound is so
 // loose (> 2^13) that some residual terms fall below fp16's normal range.
 __device__ __forceinline__ void x3_scale_from(float U, int kw, float& isc, float& us, float& ius) {
-  const int e = max(__builtin_amdgcn_frexp_expf(U), -60);
+  // a bound that overflowed (R * max |a| + B > FLT_MAX while the values are
+  // finite) would give frexp's exponent 0 for inf and a 2^14 scale: clamp it,
+  // so the scale stays at or above every finite value's
+  const int e = max(__builtin_amdgcn_frexp_expf(fminf(U, 3.40282347e38f)), -60);
   isc = __builtin_amdgcn_ldexpf(kSwishPrescale, e - 14);
   us = __builtin_amdgcn_ldexpf(1.0f, e - 14 - kw);
   ius = __builtin_amdgcn_ldexpf(1.0f, 14 + kw - e);
@@ -1796,8 +1799,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #endif
           RqsBin bin;
           bool binned = false;
-          if constexpr (ZF_X3_BSEARCH && !kSplitWH && (K == 8 || K == 16 || K == 32 || K == 64)) {
-            if (klit) {  // the halving search takes unpadded knots only
+          if constexpr (ZF_X3_BSEARCH && !kSplitWH && !kPreSP && (K == 8 || K == 16 || K == 32 || K == 64)) {
+            if (klit) {  // the halving search takes unpadded knots only, not yet squareplus'd ones
               bin = x3_bin<!INV, K, OACT, true>(xv, P, kc);
               binned = true;
             }

@@ -196,8 +196,8 @@ def _wrap_method(fn):
                 _adopt(s, self)
         s.stack.append(self)
         try:
+            self._ensure_setup()  # once per init/apply call
             if s.initializing:
-                self._ensure_setup()
                 for name in list(self.__dict__.get("_zf_refs", {})):
                     getattr(self, name)  # flax creates setup()'s variables at init
             return fn(self, *args, **kwargs)
@@ -214,8 +214,8 @@ _NOT_WRAPPED = {"init", "apply", "param", "variable", "setup", "bind"}
 class _SetupRef:
     """What ``self.param`` / ``self.variable`` return inside ``setup()``: a
     declaration, bound to the variables of whichever init/apply call reads
-    the attribute (flax re-runs setup per bind; here setup runs once and its
-    declarations resolve per call)."""
+    the attribute (setup() itself re-runs per init/apply call, as flax
+    re-runs it per bind: ``Module._ensure_setup``)."""
 
     def __init__(self, kind, args):
         self.kind, self.args = kind, args
@@ -243,6 +243,42 @@ class _SetupRef:
 
     def __repr__(self):
         return f"<{self.kind} {self.args[0]!r} declared in setup()>"
+
+
+def _same_value(a, b) -> bool:
+    if a is b:
+        return True
+    if isinstance(a, Module) or isinstance(b, Module):
+        return _same_module_config(a, b)
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        return type(a) is type(b) and len(a) == len(b) and all(_same_value(x, y) for x, y in zip(a, b))
+    if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+        return (isinstance(a, np.ndarray) and isinstance(b, np.ndarray) and a.dtype == b.dtype
+                and a.shape == b.shape and bool(np.array_equal(a, b)))
+    if (type(a) is type(b) and not callable(a) and hasattr(a, "__dict__")
+            and type(a).__eq__ is object.__eq__):  # plain config objects (a latent distribution)
+        va = {k: v for k, v in vars(a).items() if not k.startswith("_")}  # lazily set state (Distribution._dim)
+        vb = {k: v for k, v in vars(b).items() if not k.startswith("_")}
+        return va.keys() == vb.keys() and all(_same_value(va[k], vb[k]) for k in va)
+    try:
+        return bool(a == b)
+    except Exception:
+        return False
+
+
+def _same_module_config(a, b) -> bool:
+    """Two modules (or lists of modules) of one class with equal public
+    attributes: the instance a setup() re-run may keep."""
+    if isinstance(a, (list, tuple)) or isinstance(b, (list, tuple)):
+        return (isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)) and len(a) == len(b)
+                and all(isinstance(x, Module) for x in a) and all(_same_module_config(x, y) for x, y in zip(a, b)))
+    if not (isinstance(a, Module) and isinstance(b, Module)) or type(a) is not type(b):
+        return False
+    # constructor configuration only: what a's own setup() derived is not
+    sa, sb = a.__dict__.get("_zf_setup_attrs", ()), b.__dict__.get("_zf_setup_attrs", ())
+    pa = {k: v for k, v in a.__dict__.items() if not k.startswith("_") and k not in sa}
+    pb = {k: v for k, v in b.__dict__.items() if not k.startswith("_") and k not in sb}
+    return pa.keys() == pb.keys() and all(_same_value(pa[k], pb[k]) for k in pa)
 
 
 def _resolve_method(module, method):
@@ -283,9 +319,12 @@ class Module:
                 setattr(cls, name, _wrap_method(fn))
 
     def __setattr__(self, name, value):
+        d = self.__dict__
+        if d.get("_zf_in_setup") and not name.startswith("_"):
+            d.setdefault("_zf_setup_attrs", set()).add(name)
         if isinstance(value, _SetupRef):  # self.w = self.param(...) in setup()
-            self.__dict__.setdefault("_zf_refs", {})[name] = value
-            self.__dict__.pop(name, None)
+            d.setdefault("_zf_refs", {})[name] = value
+            d.pop(name, None)
             return
         object.__setattr__(self, name, value)
         if not name.startswith("_"):
@@ -303,14 +342,36 @@ class Module:
         raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
 
     def _ensure_setup(self) -> None:
+        """Run setup() once per init/apply call (flax re-runs it on every
+        bind), so attributes it derives from param values (``self.w2 =
+        self.w * 2``) follow the variables of the current call.
+        Outside any call it runs once, lazily.  A submodule that a re-run
+        creates again with the same configuration keeps the previous instance,
+        so per-instance device-program caches survive repeated apply calls."""
         d = self.__dict__
-        if not d.get("_zf_setup_done") and callable(getattr(type(self), "setup", None)):
-            d["_zf_setup_done"] = True
-            d["_zf_in_setup"] = True
-            try:
-                self.setup()
-            finally:
-                d["_zf_in_setup"] = False
+        if not callable(getattr(type(self), "setup", None)):
+            return
+        s = getattr(_tls, "scope", None)
+        key = None if s is None else s.serial
+        if d.get("_zf_setup_done") and (key is None or d.get("_zf_setup_serial") == key):
+            return
+        old = {}
+        if d.get("_zf_setup_done"):
+            for name in d.pop("_zf_setup_attrs", ()):
+                if name in d:
+                    old[name] = d.pop(name)
+            d.pop("_zf_refs", None)
+        d["_zf_setup_done"] = True
+        d["_zf_setup_serial"] = key
+        d["_zf_in_setup"] = True
+        try:
+            self.setup()
+        finally:
+            d["_zf_in_setup"] = False
+        for name, prev in old.items():
+            if name in d and _same_module_config(prev, d[name]):
+                object.__setattr__(self, name, prev)
+                _name_children(self, name, prev)
 
     def init(self, rng, *args, method=None, **kwargs) -> Dict[str, Any]:
         """Create the variables (``params`` + ``batch_stats``) for the input shapes.
