@@ -312,25 +312,25 @@ CENTERED_ACTS = ["sigmoid", "softplus", "mixed_fp32"]
 def test_kernel_selection(name, monkeypatch):
     """Every activation runs on f16x2 (relu, leaky_relu, tanh, gelu and elu
     through the activation switch, sigmoid and softplus centred); under
-    ZF_X3_SCHEME=bf16x3 every activation but softplus runs on bf16x3 and
-    softplus on the fp32 kernel (x3_eligible).  Knot counts other than
-    8 / 16 / 32 (up to 32) run padded (PADK_SHAPES)."""
+    ZF_X3_SCHEME=bf16x3 swish flows run on bf16x3 and the other activations
+    on the fp32 kernel (x3_eligible: bf16x3 is built for swish only, round 6).
+    Knot counts other than 8 / 16 / 32 (up to 32) run padded (PADK_SHAPES)."""
     case = make_case(name, N=8, seed=30)
     _, bf = _bound(case)
     assert bf.program.kernel_variant == "f16x2"
     monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == ("fp32" if name == "softplus" else "bf16x3")
+    assert bf.program.kernel_variant == ("fp32" if name in ACTS else "bf16x3")
 
 
-@pytest.mark.parametrize("name", [a for a in ACTS if a != "softplus"])
+@pytest.mark.parametrize("name", ACTS)
 def test_bf16x3_activation_parity(name, monkeypatch):
-    """NeuralSplineCoupling.act (bijectors.py:319, 345) on the bf16x3 split
-    kernel (ZF_X3_SCHEME=bf16x3)."""
+    """NeuralSplineCoupling.act (bijectors.py:319, 345) other than swish under
+    ZF_X3_SCHEME=bf16x3: the fp32 kernel takes them, at the oracle's parity."""
     monkeypatch.setenv("ZF_X3_SCHEME", "bf16x3")
     case = make_case(name, N=3000, seed=37)
     _, bf = _bound(case)
-    assert bf.program.kernel_variant == "bf16x3"
+    assert bf.program.kernel_variant == "fp32"
     check_lp(gpu_log_prob(case), case, f"bf16x3/{name}")
     rng = np.random.default_rng(38)
     z = (0.5 + 0.1 * rng.standard_normal(case["x"].shape)).astype(F32)
@@ -586,6 +586,57 @@ def test_cfg4_excess_rows_shared_by_every_scheme(monkeypatch):
     worst = int(e["f16x2"].argmax())
     assert e["f16x2"].max() <= max(e["fp32"].max(), e["bf16x3"].max())
     assert e["fp32"][worst] > eo_max and e["bf16x3"][worst] > eo_max
+
+
+def test_trained_cfg1_strict_excess_is_the_oracles_rounding(monkeypatch):
+    """on the trained cfg1 weights f16x2 leaves 1e-5 of the
+    fp32 ORACLE on some rows (2.3e-5 at most) where the unsplit fp32 kernel
+    stays within 1.2e-5.  Row by row against the exact (fp64) answer: every
+    such row is ill-conditioned (~4 ulp of noise in the fp32 intermediates
+    moves its log_prob by more than WELL_CONDITIONED), f16x2 sits within the
+    row's conditioning of fp64 there, and over all rows f16x2's error vs fp64
+    is no larger than the fp32 oracle's own (max and mean) nor than the fp32
+    kernel's max — the excess is the oracle's rounding, not the split's.
+    Record: strict_rows.jsonl (profiles/r06_trained_cfg1_rows.json)."""
+    from pathlib import Path
+
+    from zenflow_amd.io import load_variables
+
+    g = Path(__file__).parent / "golden"
+    d = np.load(g / "trained_cfg1_data.npz")
+    base = make_case("cfg1", N=1, seed=0)
+    case = dict(base, variables=load_variables(g / "trained_cfg1.npz"), x=d["x"], c=None)
+    lp = {}
+    for scheme in ["f16x2", "fp32"]:
+        monkeypatch.delenv("ZF_DISABLE_X3", raising=False)
+        if scheme == "fp32":
+            monkeypatch.setenv("ZF_DISABLE_X3", "1")
+        _, bf = _bound(case)
+        assert bf.program.kernel_variant == scheme
+        lp[scheme] = gpu_log_prob(case)
+    r32, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], None)
+    r64, _ = O.flow_log_prob(case["model"], case["variables"], case["x"], None, dtype=np.float64)
+    sens = O.row_sensitivity(case["model"], case["variables"], case["x"], None)
+    f = np.isfinite(r64) & np.isfinite(r32) & np.isfinite(lp["f16x2"]) & np.isfinite(lp["fp32"])
+    assert f.mean() > 0.99
+    sc = np.maximum(1.0, np.abs(r64[f]))
+    e = {k: np.abs(v[f] - r64[f]) / sc for k, v in lp.items()}
+    eo = np.abs(r32[f] - r64[f]) / sc
+    s_r = sens[f] / sc
+    strict = np.abs(lp["f16x2"][f].astype(np.float64) - r32[f]) / np.maximum(1.0, np.abs(r32[f]))
+    over = np.where(strict > REL)[0]
+    _append_record("strict_rows.jsonl", {"case": "trained_cfg1", "rows_over_1e-5_of_oracle32": int(over.size),
+                                         "strict_max": float(strict.max()), "f16x2_max_vs_fp64": float(e["f16x2"].max()),
+                                         "fp32_kernel_max_vs_fp64": float(e["fp32"].max()),
+                                         "oracle32_max_vs_fp64": float(eo.max()),
+                                         "f16x2_mean_vs_fp64": float(e["f16x2"].mean()),
+                                         "oracle32_mean_vs_fp64": float(eo.mean()),
+                                         "rows": [[int(np.where(f)[0][i]), float(strict[i]), float(e["f16x2"][i]),
+                                                   float(eo[i]), float(s_r[i])] for i in over]})
+    assert np.all(s_r[over] > WELL_CONDITIONED), s_r[over]
+    assert np.all(e["f16x2"][over] <= s_r[over]), (e["f16x2"][over], s_r[over])
+    assert e["f16x2"].max() <= eo.max() and e["f16x2"].max() <= e["fp32"].max()
+    assert e["f16x2"].mean() <= eo.mean()
 
 
 @pytest.mark.parametrize("scheme", ["f16x2", "bf16x3", "fp32"])

@@ -21,7 +21,7 @@ LIB = HERE / "libzenflow_amd.so"
 ARCH = os.environ.get("ZF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["zf_runtime.hip", "zf_rqs.hip", "zf_flow.hip", "zf_flow_x3.hip", "zf_flow_x3_k8.hip", "zf_flow_x3_k16.hip", "zf_flow_x3_k32.hip", "zf_flow_x3_k64.hip", "zf_flow_x3_k64_act.hip", "zf_flow_x3_k8_act.hip", "zf_flow_x3_k16_act.hip", "zf_flow_x3_k32_act.hip", "zf_flow_x3_k8_act1.hip", "zf_flow_x3_k16_act1.hip", "zf_flow_x3_k32_act1.hip", "zf_flow_x3_k8_act2.hip", "zf_flow_x3_k16_act2.hip", "zf_flow_x3_k32_act2.hip", "zf_stats.hip", "zf_rccl.hip", "zf_train.hip", "zf_layered.hip"]
+SOURCES = ["zf_runtime.hip", "zf_rqs.hip", "zf_flow.hip", "zf_flow_x3.hip", "zf_flow_x3_k8.hip", "zf_flow_x3_k16.hip", "zf_flow_x3_k32.hip", "zf_flow_x3_k64.hip", "zf_flow_x3_k64_act.hip", "zf_flow_x3_k8_act.hip", "zf_flow_x3_k16_act.hip", "zf_flow_x3_k32_act.hip", "zf_flow_x3_k8_act2.hip", "zf_flow_x3_k16_act2.hip", "zf_flow_x3_k32_act2.hip", "zf_stats.hip", "zf_rccl.hip", "zf_train.hip", "zf_layered.hip"]
 HEADERS = sorted(p.name for p in CSRC.glob("*.h"))
 
 FLAGS = [

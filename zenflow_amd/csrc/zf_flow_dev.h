@@ -357,7 +357,7 @@ struct X3Launch {
   int K, D, C, T;  // knots, dim, conditions, hidden tiles (4: width <= 128, 8: <= 256)
   int NT;       // split scheme: 3 = bf16x3, 2 = f16x2
   bool oact;    // some coupling's activation is not swish (f16x2 kernels with act switch)
-  int aset;     // oact, f16x2: 1 = only relu/tanh/gelu/elu/leaky_relu, 2 = only sigmoid/softplus, 0 = both kinds
+  int aset;     // oact, f16x2: 2 = only sigmoid/softplus (the _act2 units), 1 = only relu/tanh/gelu/elu/leaky_relu, 0 = both kinds (1 and 0: the full switch)
   int par_bytes;  // DevFlow::x3_par_bytes
   hipStream_t stream;
 };

@@ -59,6 +59,11 @@ bool x3_eligible(const zf_flow_desc& desc, int HP, int* K_out) {
     // fp32 oracle's (profiles/r03_diag_acts.jsonl; held by
     // tests/test_gpu_flow.py::test_split_scaling_extremes_other_acts).
     if (op.act == ZF_ACT_SOFTPLUS && x3_scheme() == 3) return false;
+    // bf16x3 (the scaling-free reference scheme) is instantiated for swish
+    // couplings only: its activation-switch builds were 10 MB of the library
+    // for an opt-in scheme, so other activations there run the fp32 kernel
+    // 
+    if (op.act != ZF_ACT_SWISH && x3_scheme() == 3) return false;
     // a chain may mix knot counts: all run at the largest one's
     // instantiation; a 1-knot coupling anywhere keeps the flow off it, as a
     // flow of 1-knot couplings is (that case is not pinned)

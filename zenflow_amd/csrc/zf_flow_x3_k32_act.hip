@@ -1,21 +1,23 @@
 // Split-MFMA fused flow kernel instantiations for K = 32 knots with
-// NeuralSplineCoupling activations other than swish (both schemes; own
+// NeuralSplineCoupling activations other than swish (f16x2 only; own
 // translation unit so the swish build is untouched and both compile in
 // parallel).
 #include "zf_flow_x3_kernel.h"
 
 namespace zf {
 
-int launch_x3_k32_act1(const X3Launch& a, bool inverse);
 int launch_x3_k32_act2(const X3Launch& a, bool inverse);
 
-// f16x2 flows whose activations are all of one kind get the narrower
-// instantiations (zf_flow_x3_k32_act1 / _act2: the other kind's code out of
-// the register budget); mixed flows and bf16x3 take the full switch here.
+// f16x2 flows whose activations are all sigmoid / softplus (centred) get the
+// narrower instantiation zf_flow_x3_k32_act2 (their activation inside the
+// group steps: sigmoid 0.85 -> 1.03 G samples/s); every other activation runs
+// the full switch here (a relu / tanh / gelu / elu / leaky_relu-only set
+// measured 0.5-2% slower than this one and was retired in round 6:
+// profiles/r06_aset_ab.txt).
 int launch_x3_k32_act(const X3Launch& a, bool inverse) {
-  if (a.NT == 2 && a.aset == 1) return launch_x3_k32_act1(a, inverse);
   if (a.NT == 2 && a.aset == 2) return launch_x3_k32_act2(a, inverse);
-  return a.NT == 2 ? launch_x3_k<2, 32, true>(a, inverse) : launch_x3_k<3, 32, true>(a, inverse);
+  return a.NT == 2 ? launch_x3_k<2, 32, true>(a, inverse)
+                   : enotsup("bf16x3 takes swish couplings only (x3_eligible)");
 }
 
 }  // namespace zf

@@ -243,7 +243,9 @@ constexpr float kLn2 = 0.693147180559945309f;
 __device__ __forceinline__ float act_sigmoid_centered(float v) {
   // 1 / (1 + 2^(-v log2 e)) with a residual-corrected reciprocal (as the
   // bf16x3 form); 1 + e = inf (v < -88) gives 0.  |v| < 1/4: tanh(v/2)/2 =
-  // v/4 - v^3/48 + v^5/480 - 17 v^7/80640
+  // v/4 - v^3/48 + v^5/480 - 17 v^7/80640.  (Round 6 measured a form with a
+  // clamped exponent and no inf / NaN tests 3% SLOWER at cfg2's shape:
+  // profiles/r06_act_ab.txt.)
   const float d = 1.0f + __builtin_amdgcn_exp2f(-v * kSwishPrescale);
   const float q = __builtin_amdgcn_rcpf(d);
   const float sg = __builtin_fmaf(q, __builtin_fmaf(-d, q, 1.0f), q);
@@ -253,18 +255,22 @@ __device__ __forceinline__ float act_sigmoid_centered(float v) {
                          0.25f);
   return fabsf(v) < 0.25f ? ser : (d == __builtin_huge_valf() ? 0.0f : sg) - 0.5f;
 }
+// softplus (round 6; 7% faster at cfg2's shape,
+// profiles/r06_act_ab.txt): the select tests |v| >= 1/4, false for NaN, so a
+// NaN input takes the series branch and stays NaN without a compare of its
+// own; log1p's small-t series is gone: a centred value a = softplus(v) -
+// log 2 carries t = exp(-|v|) < 1/64 only at |v| > 4.2, where 1 + t's
+// rounding (2^-24 absolute) is below a's own ulp.
 __device__ __forceinline__ float act_softplus_centered(float v) {
-  // logaddexp(v, 0) = max(v, 0) + log1p(exp(-|v|)): log1p from the hardware
-  // log2 of 1 + t, or its series below t = 1/64 (where 1 + t loses t's bits).
+  // logaddexp(v, 0) - log 2 = max(v, 0) + log1p(exp(-|v|)) - log 2, log1p
+  // from the hardware log2 of 1 + t.
   // |v| < 1/4: softplus(v) - log 2 = v/2 + v^2/8 - v^4/192 + v^6/2880
   const float t = __builtin_amdgcn_exp2f(-fabsf(v) * kSwishPrescale);
-  const float lg = __builtin_amdgcn_logf(1.0f + t) * kLn2;
-  const float ls = t * __builtin_fmaf(t, __builtin_fmaf(t, __builtin_fmaf(t, -0.25f, 1.0f / 3.0f), -0.5f), 1.0f);
-  const float sp = fmaxf(v, 0.0f) + (t < 0.015625f ? ls : lg);
+  const float sp = __builtin_fmaf(__builtin_amdgcn_logf(1.0f + t), kLn2, fmaxf(v, 0.0f));
   const float v2 = v * v;
   const float ser = v * __builtin_fmaf(v, __builtin_fmaf(v2, __builtin_fmaf(v2, 1.0f / 2880.0f, -1.0f / 192.0f), 0.125f),
                                        0.5f);
-  return fabsf(v) < 0.25f ? ser : (v != v ? v : sp - kLn2);
+  return fabsf(v) >= 0.25f ? sp - kLn2 : ser;
 }
 
 template <int CODE>

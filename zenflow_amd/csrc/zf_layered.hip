@@ -239,7 +239,8 @@ int layered_run(LayeredFlow* L, const DevFlow& F, const float* packed, bool inve
         const bool last = l == op.n_hidden;
         const int out_w = last ? d.dt * d.S : op.hidden[l];
         float* H = (l & 1) ? L->H1 : L->H0;
-        rc = dense_gemm(n, n, out_w, in_w, in, in_w, L->d_nat + op.off_w[l], out_w, last ? L->P : L->Z, out_w,
+        // hidden layers keep only the activation H (no pre-activation store: eval has no backward)
+        rc = dense_gemm(n, n, out_w, in_w, in, in_w, L->d_nat + op.off_w[l], out_w, last ? L->P : nullptr, out_w,
                         last ? nullptr : H, st, L->d_nat + op.off_b[l], op.act);
         if (rc) return rc;
         in = H;

@@ -15,17 +15,8 @@
 
 #include <cstdlib>
 
-#ifndef ZF_K1_1LOG
-#define ZF_K1_1LOG 1  // forward log-det as one log (rqs_forward_eval_1log); 0: three logs
-#endif
-
 namespace zf {
 namespace {
-
-__device__ __forceinline__ void k1_forward_eval(float x, const RqsBin& b, float& y, float& ld) {
-  if constexpr (ZF_K1_1LOG) rqs_forward_eval_1log(x, b, y, ld);
-  else rqs_forward_eval(x, b, y, ld);
-}
 
 constexpr int kK1Threads = 256;
 constexpr int kK1LdsBudgetFloats = 12288;  // 48 KiB per block
@@ -107,7 +98,7 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel(
     const RqsBin b = rqs_bin<FWD>(v, K, p);
     if (FWD) {
       float y, ld;
-      k1_forward_eval(v, b, y, ld);
+      rqs_forward_eval(v, b, y, ld);
       if (out) out[item0 + i] = y;
       s_ld[i] = ld;
     } else {
@@ -172,7 +163,7 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_direct(
   }
   if (FWD) {
     float y, l;
-    k1_forward_eval(v, bn, y, l);
+    rqs_forward_eval(v, bn, y, l);
     if (tid < items && out) out[item] = y;
     if (log_det) {
       if (N <= 64 && (N & (N - 1)) == 0) {
@@ -284,7 +275,7 @@ __global__ __launch_bounds__(kK1Threads) void rqs_kernel_pair(
   }
   if (FWD) {
     float y, l;
-    k1_forward_eval(v, b, y, l);
+    rqs_forward_eval(v, b, y, l);
     if (p == 0 && it < items && out) out[item] = y;
     if (log_det) {
       if (N <= 32 && (N & (N - 1)) == 0) {

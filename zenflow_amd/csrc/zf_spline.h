@@ -342,32 +342,6 @@ __device__ __forceinline__ void rqs_forward_eval(float x, const RqsBin& b, float
   ld = b.oob ? 0.0f : l;                                            // :138
 }
 
-// rqs_forward_eval with the log-det as ONE log (K1):
-// 2 log(sk+eps) + log(num2+eps) - 2 log(den+eps) = log((num2+eps) q^2),
-// q = (sk+eps)/(den+eps) (utils.py:133-135, EPS placement kept).  den >=
-// sk/2, so q <= ~2 and the product overflows only where num2 itself is near
-// FLT_MAX; where it leaves the normal range (over- or underflow: slopes far
-// apart in magnitude) the three-log form runs instead, per lane.
-__device__ __forceinline__ void rqs_forward_eval_1log(float x, const RqsBin& b, float& y, float& ld) {
-  const float zr = (x - b.xk) / b.w;               // :122
-  const float z = (zr != zr) ? zr : fminf(fmaxf(zr, kEps), kOneMinusEps);
-  const float az = 1.0f - z;
-  const float num = b.h * z * (b.sk * z + b.dk * az);              // :125
-  const float den = b.sk + (b.dkp1 + b.dk - 2.0f * b.sk) * z * az;  // :126
-  const float yv = b.yk + num / (den + kEps);                       // :127
-  y = b.oob ? x : yv;                                               // :130
-  const float num2 = z * (b.dkp1 * z + 2.0f * b.sk * az) + b.dk * (az * az);  // :133
-  const float q = (b.sk + kEps) / (den + kEps);
-  const float p = (num2 + kEps) * (q * q);
-  float l;
-  if (__builtin_expect(p >= 1.17549435e-38f && p <= 3.40282347e38f, 1)) {
-    l = logf(p);
-  } else {
-    l = 2.0f * logf(b.sk + kEps) + logf(num2 + kEps) - 2.0f * logf(den + kEps);
-  }
-  ld = b.oob ? 0.0f : l;                                            // :138
-}
-
 // utils.py:191-201 — inverse via the quadratic root.
 __device__ __forceinline__ float rqs_inverse_eval(float y, const RqsBin& b) {
   const float dy = y - b.yk;

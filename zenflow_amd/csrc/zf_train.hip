@@ -70,7 +70,7 @@ __device__ __forceinline__ void gemm_epilogue(float v, int n, long long o, float
       v = v * act_other_grad(act, z);
     }
   }
-  C[o] = v;
+  if (C) C[o] = v;  // null: the eval path keeps only the activation H
 }
 
 // The same for four consecutive columns n..n+3 (n % 4 == 0 < N, N % 4 == 0,
@@ -104,7 +104,7 @@ __device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, flo
       }
     }
   }
-  *reinterpret_cast<float4*>(C + o) = float4{x[0], x[1], x[2], x[3]};
+  if (C) *reinterpret_cast<float4*>(C + o) = float4{x[0], x[1], x[2], x[3]};
 }
 
 // SPLITQ: block z = q of a 64 x 64 tile multiplies only the k-pairs
@@ -308,6 +308,49 @@ __global__ void gemm_small_k_kernel(int M, int N, int K, const float* __restrict
   }
   const float v = (__fadd_rn(sq[0], 0.f) + __fadd_rn(sq[1], 0.f)) + (__fadd_rn(sq[2], 0.f) + __fadd_rn(sq[3], 0.f));
   gemm_epilogue(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+}
+
+// gemm_small_k_kernel with four consecutive outputs per thread (N % 4 == 0,
+// 16-B aligned C / H rows): the same fma order per output (the same bits),
+// the A row read once for four columns, and one dwordx4 store per array
+// instead of four dword stores — the kernel is bound by its Z / H stores
+// (2^17 x 512 outputs: 200 us as one thread per output on the layered eval
+// path, profiles/r06_layered_kernel_stats.csv).
+__global__ void gemm_small_k4_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                     const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc, int epi,
+                                     const float* __restrict__ bias, float* __restrict__ H, int act) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int N4 = N >> 2;
+  if (i >= (long long)M * N4) return;
+  const int m = (int)(i / N4), n = 4 * (int)(i - (long long)m * N4);
+  float a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = k < K ? A[(long long)m * lda + k] : 0.f;
+  float out[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int k = 2 * p;
+      if (k < K) {
+        const float b0 = B[(long long)k * ldb + n + t];
+        const float b1 = k + 1 < K ? B[(long long)(k + 1) * ldb + n + t] : 0.f;
+        sq[p] = __builtin_fmaf(a[k + 1], b1, __builtin_fmaf(a[k], b0, sq[p]));
+      }
+    }
+    float v = (__fadd_rn(sq[0], 0.f) + __fadd_rn(sq[1], 0.f)) + (__fadd_rn(sq[2], 0.f) + __fadd_rn(sq[3], 0.f));
+    if (epi == kEpiBias) v = v + bias[n + t];
+    out[t] = v;
+  }
+  const long long o = (long long)m * ldc + n;
+  if (epi == kEpiBias && H) {
+    float y[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) y[t] = act == ZF_ACT_SWISH ? out[t] * sigmoidf(out[t]) : act_other(act, out[t]);
+    *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+  }
+  if (C) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
 }
 
 // ---- Large-batch GEMMs on bf16x3 split MFMA ----------------------------------
@@ -549,6 +592,13 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     // 32-deep k-tile of zeros (the choice follows the global batch, as below;
     // not a split-set form, so ZF_TRAIN_SPLITQ=0 keeps it)
     const long long MN = (long long)M * N;
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (N % 4 == 0 && ldc % 4 == 0 && al16(C) && al16(H) && (epi == kEpiBias || epi == kEpiNone)) {
+      hipLaunchKernelGGL(gemm_small_k4_kernel, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st, M, N, K, A,
+                         lda, B, ldb, C, ldc, epi, bias, H, act);
+      ZF_CHECK_LAUNCH("gemm_small_k4_kernel");
+      return ZF_OK;
+    }
     hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
                        ldb, C, ldc, epi, bias, H, Z, act);
     ZF_CHECK_LAUNCH("gemm_small_k_kernel");
