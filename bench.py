@@ -40,6 +40,7 @@ SPLIT_PEAKS = {
     "f16x2": (PEAK_F16X2_TFLOPS, "fp16 dense MFMA peak / 3 (two-term fp16 split, fp32-equivalent flops)"),
 }
 PEAK_HBM_GBS = 8000.0
+PEAK_CLOCK_GHZ = 2.4  # the clock every MFMA peak above assumes
 
 WORKLOADS = {
     # name: (D, C, K, layers, couplings, latent, mode)
@@ -542,6 +543,9 @@ def main():
     peak, peak_basis = SPLIT_PEAKS.get(variant, (PEAK_FP32_MFMA_TFLOPS, "fp32 dense MFMA peak"))
     pmc = load_pmc(kernel_name) if rank == 0 else {}
     traffic = pmc.get("hbm_bytes_per_launch")
+    held_ghz = None
+    if pmc.get("kernel_cycles") and pmc.get("avg_duration_us_trace"):
+        held_ghz = pmc["kernel_cycles"] / (pmc["avg_duration_us_trace"] * 1e3)
     result = {
         "metric": "log_prob samples/sec (+ NLL match) 4D 16-knot 4-layer flow, batch 2^20"
         if name == "cfg2" else ("log_prob samples/sec through Flow.apply (host in/out)" if mode == "apply"
@@ -572,6 +576,12 @@ def main():
             "peak_basis": peak_basis,
             "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
             "mfma_busy": pmc.get("mfma_busy"),
+            # the shader clock the kernel held in the committed counter pass
+            # (GRBM_GUI_ACTIVE / 8 XCDs per launch / the trace's average
+            # duration) and frac at that clock: frac = mfma-pipe share x the
+            # clock ratio (the peak assumes 2.4 GHz)
+            "held_clock_ghz": held_ghz,
+            "frac_at_held_clock": (achieved / peak) * (PEAK_CLOCK_GHZ / held_ghz) if held_ghz else None,
             "valu_active": pmc.get("valu_active"),
             "valu_mfma_coexec": pmc.get("valu_mfma_coexec"),
             "pmc_source": pmc.get("source"),

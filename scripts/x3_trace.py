@@ -32,9 +32,10 @@ fn = getattr(lib, f"zf_x3_trace_set_k{K}")
 fn.argtypes = [C.c_void_p]
 assert fn(buf.ptr) == 0
 xd = DeviceArray.from_numpy(x)
+cd = DeviceArray.from_numpy(c) if c is not None else None  # conditional flows (cfg4)
 out = DeviceArray((N,))
 for _ in range(5):
-    prog.log_prob(xd, None, out=out)
+    prog.log_prob(xd, cd, out=out)
 L.synchronize()
 t = buf.numpy().reshape(nwaves, 16).astype(np.float64)
 names = ["start->nsc", "layer0", "hidden", "hid->last", "last", "spline", "epilogue", "barrier_wait", "total",

@@ -80,11 +80,13 @@ __device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, flo
                                                const float* __restrict__ Z, int act) {
   float x[4] = {v.x, v.y, v.z, v.w};
   if (epi == kEpiBias) {
-    const float4 b = *reinterpret_cast<const float4*>(bias + n);
-    x[0] = x[0] + b.x;
-    x[1] = x[1] + b.y;
-    x[2] = x[2] + b.z;
-    x[3] = x[3] + b.w;
+    // four scalar loads: a Dense bias inside the natural blob need not be
+    // 16-B aligned (the layered path's biases alternate), and the WIDE
+    // epilogue should not depend on it
+    x[0] = x[0] + bias[n];
+    x[1] = x[1] + bias[n + 1];
+    x[2] = x[2] + bias[n + 2];
+    x[3] = x[3] + bias[n + 3];
     if (H) {
       float y[4];
 #pragma unroll
@@ -310,47 +312,53 @@ __global__ void gemm_small_k_kernel(int M, int N, int K, const float* __restrict
   gemm_epilogue(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
 }
 
-// gemm_small_k_kernel with four consecutive outputs per thread (N % 4 == 0,
-// 16-B aligned C / H rows): the same fma order per output (the same bits),
-// the A row read once for four columns, and one dwordx4 store per array
-// instead of four dword stores — the kernel is bound by its Z / H stores
-// (2^17 x 512 outputs: 200 us as one thread per output on the layered eval
-// path, profiles/r06_layered_kernel_stats.csv).
-__global__ void gemm_small_k4_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+// gemm_small_k_kernel with four consecutive outputs of kSk4Rows rows per
+// thread (N % 4 == 0, 16-B aligned C / H rows): the same fma order per
+// output (the same bits), the B columns and bias read once for all rows,
+// and one dwordx4 store per array and row.  Grid (ceil(N / 256),
+// ceil(M / (4 kSk4Rows))), block (64, 4): no per-thread division.
+constexpr int kSk4Rows = 8;
+__global__ __launch_bounds__(256) void gemm_small_k4_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                      const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc, int epi,
                                      const float* __restrict__ bias, float* __restrict__ H, int act) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int N4 = N >> 2;
-  if (i >= (long long)M * N4) return;
-  const int m = (int)(i / N4), n = 4 * (int)(i - (long long)m * N4);
-  float a[8];
+  const int m0 = (blockIdx.y * 4 + threadIdx.y) * kSk4Rows;
+  const int n = 4 * (blockIdx.x * 64 + threadIdx.x);
+  if (m0 >= M || n >= N) return;
+  float b[8][4], bs[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) a[k] = k < K ? A[(long long)m * lda + k] : 0.f;
-  float out[4];
+  for (int k = 0; k < 8; ++k)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 4; ++t) b[k][t] = k < K ? B[(long long)k * ldb + n + t] : 0.f;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int k = 2 * p;
-      if (k < K) {
-        const float b0 = B[(long long)k * ldb + n + t];
-        const float b1 = k + 1 < K ? B[(long long)(k + 1) * ldb + n + t] : 0.f;
-        sq[p] = __builtin_fmaf(a[k + 1], b1, __builtin_fmaf(a[k], b0, sq[p]));
+  for (int t = 0; t < 4; ++t) bs[t] = epi == kEpiBias ? bias[n + t] : 0.f;
+  for (int r = 0; r < kSk4Rows; ++r) {
+    const int m = m0 + r;
+    if (m >= M) break;
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = k < K ? A[(long long)m * lda + k] : 0.f;
+    float out[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int k = 2 * p;
+        if (k < K) sq[p] = __builtin_fmaf(a[k + 1], b[k + 1][t], __builtin_fmaf(a[k], b[k][t], sq[p]));
       }
+      float v = (__fadd_rn(sq[0], 0.f) + __fadd_rn(sq[1], 0.f)) + (__fadd_rn(sq[2], 0.f) + __fadd_rn(sq[3], 0.f));
+      if (epi == kEpiBias) v = v + bs[t];
+      out[t] = v;
     }
-    float v = (__fadd_rn(sq[0], 0.f) + __fadd_rn(sq[1], 0.f)) + (__fadd_rn(sq[2], 0.f) + __fadd_rn(sq[3], 0.f));
-    if (epi == kEpiBias) v = v + bias[n + t];
-    out[t] = v;
-  }
-  const long long o = (long long)m * ldc + n;
-  if (epi == kEpiBias && H) {
-    float y[4];
+    const long long o = (long long)m * ldc + n;
+    if (epi == kEpiBias && H) {
+      float y[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) y[t] = act == ZF_ACT_SWISH ? out[t] * sigmoidf(out[t]) : act_other(act, out[t]);
-    *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+      for (int t = 0; t < 4; ++t) y[t] = act == ZF_ACT_SWISH ? out[t] * sigmoidf(out[t]) : act_other(act, out[t]);
+      *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+    }
+    if (C) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
   }
-  if (C) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
 }
 
 // ---- Large-batch GEMMs on bf16x3 split MFMA ----------------------------------
@@ -416,10 +424,17 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
   const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 64;
   int m0 = 0, n0 = 0;  // the current output tile (the loop below)
   const int r = lane & 31, h = lane >> 5;
+  // Register staging of one k-tile: A rows (and B rows when TB) as float4s,
+  // B columns as scalars (!TB).  Two sets, filled two k-tiles ahead of the
+  // MFMAs that consume them — across output-tile boundaries too, so neither
+  // a tile's first k-tile nor any other waits on a full memory latency
+  // (one set, one k-tile ahead: Dense 512 x 512 at 0.31 of the MFMA rate).
+  struct Stage {
+    float4 ra[4], rb[4];
+    float rbs[16];
+  };
   // row-major [rows][K] tiles (A; B when TB): thread -> row e >> 2 (e = tid,
   // tid + 256), 8 consecutive k at 8 (e & 3) as two float4s
-  float4 ra[4], rb[4];
-  float rbs[16];
   auto load_rows = [&](const float* P, int ld, int r0, int R, int k0, float4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -440,47 +455,101 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
     }
   };
   // B row-major [K][N] (!TB): thread -> column n0 + (tid & 127), k 16 (tid >> 7) .. +15
-  auto load_cols = [&](int k0) {
-    const int n = n0 + (tid & 127);
+  auto load_cols = [&](int tn0, int k0, float (&v)[16]) {
+    const int n = tn0 + (tid & 127);
     const int kb = k0 + 16 * (tid >> 7);
     const float* src = B + (long long)kb * ldb + n;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) rbs[j] = n < N && kb + j < K ? src[(long long)j * ldb] : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = n < N && kb + j < K ? src[(long long)j * ldb] : 0.f;
   };
-  auto store_cols = [&]() {
+  auto store_cols = [&](const float (&v)[16]) {
     __bf16* P = Bp + (tid & 127) * kX3RS + 16 * (tid >> 7);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const float x[8] = {rbs[8 * g], rbs[8 * g + 1], rbs[8 * g + 2], rbs[8 * g + 3],
-                          rbs[8 * g + 4], rbs[8 * g + 5], rbs[8 * g + 6], rbs[8 * g + 7]};
+      const float x[8] = {v[8 * g], v[8 * g + 1], v[8 * g + 2], v[8 * g + 3],
+                          v[8 * g + 4], v[8 * g + 5], v[8 * g + 6], v[8 * g + 7]};
       split3_store(x, P + 8 * g);
     }
   };
-  auto load = [&](int k0) {
-    load_rows(A, lda, m0, M, k0, ra);
-    if (TB) load_rows(B, ldb, n0, N, k0, rb);
-    else load_cols(k0);
-  };
   // persistent blocks: a block takes output tiles blockIdx.x, + gridDim.x,
   // ...; a tile's epilogue stores drain while the next tile's loads and
-  // MFMAs run (one launch round of blocks had every block storing at once)
+  // MFMAs run (one launch round of blocks had every block storing at once).
+  // The block's k-tiles in order: iteration it = tile ti (the ti-th of this
+  // block) x kt k-tiles + k-tile kk.
   const int tiles_n = (N + kX3BN - 1) / kX3BN;
   const int ntiles = tiles_n * ((M + kX3BM - 1) / kX3BM);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  m0 = (tile / tiles_n) * kX3BM;
-  n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
+  const int kt = (K + kX3BK - 1) / kX3BK;
+  const int mine = ntiles > (int)blockIdx.x ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int total = mine * kt;
+  auto load = [&](int it, Stage& st) __attribute__((always_inline)) {
+    const int ti = it / kt, k0 = (it - ti * kt) * kX3BK;
+    const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+    const int tm0 = (tile / tiles_n) * kX3BM, tn0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
+    load_rows(A, lda, tm0, M, k0, st.ra);
+    if (TB) load_rows(B, ldb, tn0, N, k0, st.rb);
+    else load_cols(tn0, k0, st.rbs);
+  };
+  Stage S0, S1;
+  if (total > 0) load(0, S0);
+  if (total > 1) load(1, S1);
   floatx16 acc[2][2];
+  auto epilogue = [&]() __attribute__((always_inline)) {
+    if (WIDE) {
+      // through LDS (free after the loop's last barrier), per wave and per
+      // 32-row half: ds_write_b128 of each lane's row pieces (row pitch 68
+      // floats: conflict-free), then row-contiguous float4s — each store
+      // instruction writes 4 rows x 256 B, whole 128-B lines
+      float* T = reinterpret_cast<float*>(lds) + wave * (32 * 68);
+  #pragma unroll
+      for (int i = 0; i < 2; ++i) {
+  #pragma unroll
+        for (int j = 0; j < 2; ++j)
+  #pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(T + r * 68 + 32 * j + 8 * g + 4 * h) =
+                float4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes
+        __builtin_amdgcn_wave_barrier();
+  #pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int row = 4 * t + (lane >> 4), c4 = lane & 15;
+          const float4 v = *reinterpret_cast<const float4*>(T + row * 68 + 4 * c4);
+          const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 4 * c4;
+          if (m < M && n < N) gemm_epilogue4(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else {
+  #pragma unroll
+      for (int i = 0; i < 2; ++i)
+  #pragma unroll
+        for (int j = 0; j < 2; ++j)
+  #pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
+            if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+          }
+    }
+    __syncthreads();  // the next tile's planes overwrite the epilogue's LDS
+  };
+  // one k-iteration from stage S (refilled with iteration it + 2 once stored)
+  auto kstep = [&](int it, Stage& S) __attribute__((always_inline)) {
+    const int ti = it / kt, kk = it - ti * kt;
+    if (kk == 0) {
+      const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+      m0 = (tile / tiles_n) * kX3BM;
+      n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += kX3BK) {
-    store_rows(Ap, ra);
-    if (TB) store_rows(Bp, rb);
-    else store_cols();
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+    }
+    store_rows(Ap, S.ra);
+    if (TB) store_rows(Bp, S.rb);
+    else store_cols(S.rbs);
     __syncthreads();
-    if (k0 + kX3BK < K) load(k0 + kX3BK);
+    if (it + 2 < total) load(it + 2, S);
 #pragma unroll
     for (int s = 0; s < kX3BK / 16; ++s) {
       tbf16x8 af[2][3], bf[2][3];
@@ -511,45 +580,11 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
         }
     }
     __syncthreads();
-  }
-  if (WIDE) {
-    // through LDS (free after the loop's last barrier), per wave and per
-    // 32-row half: ds_write_b128 of each lane's row pieces (row pitch 68
-    // floats: conflict-free), then row-contiguous float4s — each store
-    // instruction writes 4 rows x 256 B, whole 128-B lines
-    float* T = reinterpret_cast<float*>(lds) + wave * (32 * 68);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<float4*>(T + r * 68 + 32 * j + 8 * g + 4 * h) =
-              float4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int row = 4 * t + (lane >> 4), c4 = lane & 15;
-        const float4 v = *reinterpret_cast<const float4*>(T + row * 68 + 4 * c4);
-        const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 4 * c4;
-        if (m < M && n < N) gemm_epilogue4(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-          if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
-        }
-  }
-  __syncthreads();  // the next tile's planes overwrite the epilogue's LDS
+    if (kk == kt - 1) epilogue();
+  };
+  for (int it = 0; it < total; it += 2) {
+    kstep(it, S0);
+    if (it + 1 < total) kstep(it + 1, S1);
   }
 }
 
@@ -594,8 +629,8 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     const long long MN = (long long)M * N;
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     if (N % 4 == 0 && ldc % 4 == 0 && al16(C) && al16(H) && (epi == kEpiBias || epi == kEpiNone)) {
-      hipLaunchKernelGGL(gemm_small_k4_kernel, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st, M, N, K, A,
-                         lda, B, ldb, C, ldc, epi, bias, H, act);
+      hipLaunchKernelGGL(gemm_small_k4_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)((M + 4 * kSk4Rows - 1) / (4 * kSk4Rows))),
+                         dim3(64, 4), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, H, act);
       ZF_CHECK_LAUNCH("gemm_small_k4_kernel");
       return ZF_OK;
     }
@@ -611,8 +646,7 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const dim3 grid((unsigned)std::min<long long>(ntiles, 2ll * ncu));
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    const bool wide = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!H || al16(H)) && (!Z || al16(Z)) &&
-                      (!bias || al16(bias));
+    const bool wide = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!H || al16(H)) && (!Z || al16(Z));
 #define ZF_X3_LAUNCH(TB_, W_)                                                                                    \
   hipLaunchKernelGGL((gemm_x3_kernel<TB_, W_>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, \
                      H, Z, act)
