@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPO=$(pwd)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-spline-kernel ${BENCH_ARGS:-}"
+B=${PMC_CMD:-"python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-spline-kernel ${BENCH_ARGS:-}"}
 P=${PMC_PREFIX:-pmc_st}
 run() { local name=$1; shift; echo "=== $name"; timeout -s KILL 120 "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; tail -2 "gpurun_out/$name.log"; [ $rc -eq 0 ] || exit $rc; }
 run ${P}1 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d "$REPO/gpurun_out/${P}1" -o run --output-format csv -- $B
