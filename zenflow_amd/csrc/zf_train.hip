@@ -117,19 +117,11 @@ __device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, flo
 // blocks (small batches: 1024 rows give 32 tiles for 256 CUs).
 // The block body, with the block's coordinates passed in (mgemm_kernel: its
 // blockIdx; wgrad_group_kernel: decoded from one launch over several GEMMs).
-// SPLITQ with `cnt` (ZF_TRAIN_FUSED_COMBINE=1): no combine launch — each
-// split block stores its partial with agent-scope atomic stores, releases
-// it by a device-scope counter per output tile, and the fourth block to
-// arrive forms (P0 + P1) + (P2 + P3) and the epilogue into Cf / H
-// (gemm_combine_kernel's order and arithmetic: the same bits), then resets
-// the counter for the next launch.  The partials cross the XCDs' L2s through
-// the agent-scope atomics and fences only: no block placement is assumed.
 template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ>
 __device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K, const float* __restrict__ A, int lda,
                                            const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
                                            int epi, const float* __restrict__ bias, float* __restrict__ H,
-                                           const float* __restrict__ Z, int KC, int act, int* cnt = nullptr,
-                                           float* Cf = nullptr, int ldcf = 0) {
+                                           const float* __restrict__ Z, int KC, int act) {
   constexpr int NA = BM * MBK / 256, NB = BN * MBK / 256;  // tile elements per thread
   constexpr int TM = BM / 64, TN = BN / 64;                // 32x32 tiles per wave
   __shared__ float As[MBK][BM + 1];
@@ -230,42 +222,11 @@ __device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K,
   }
   if (SPLITQ) {
     float* P = C + (long long)bid.z * M * N;
-    if (cnt == nullptr) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm0 + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + r;
-        if (m < M && n < N) P[(long long)m * N + n] = acc[0][0][0][q];
-      }
-      return;
-    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int m = m0 + wm0 + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + r;
-      if (m < M && n < N)
-        __hip_atomic_store(P + (long long)m * N + n, acc[0][0][0][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m < M && n < N) P[(long long)m * N + n] = acc[0][0][0][q];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this thread's partial before the count
-    __shared__ int s_last;
-    __syncthreads();
-    int* c = cnt + bid.y * ((N + BN - 1) / BN) + bid.x;
-    if (tid == 0) s_last = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 3;
-    __syncthreads();
-    if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other three blocks' partials
-    const long long MN = (long long)M * N;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int m = m0 + wm0 + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + r;
-      if (m < M && n < N) {
-        const float* e = C + (long long)m * N + n;
-        const float p0 = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float p1 = __hip_atomic_load(e + MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float p2 = __hip_atomic_load(e + 2 * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float p3 = __hip_atomic_load(e + 3 * MN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gemm_epilogue((p0 + p1) + (p2 + p3), n, (long long)m * ldcf + n, Cf, epi, bias, H, Z, act);
-      }
-    }
-    if (tid == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch's count
     return;
   }
   if (WG) {
@@ -302,18 +263,6 @@ __device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K,
       }
 }
 
-
-// The split-set GEMM with the combine fused in (mgemm_body's cnt path).
-template <bool TB>
-__global__ __launch_bounds__(256) void mgemm_splitq_fused_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
-                                                                 const float* __restrict__ B, int ldb,
-                                                                 float* __restrict__ part, int* cnt,
-                                                                 float* __restrict__ C, int ldc, int epi,
-                                                                 const float* __restrict__ bias, float* __restrict__ H,
-                                                                 const float* __restrict__ Z, int act) {
-  mgemm_body<64, 64, false, TB, false, true>(uint3{blockIdx.x, blockIdx.y, blockIdx.z}, M, N, K, A, lda, B, ldb, part,
-                                             N, epi, bias, H, Z, 0, act, cnt, C, ldc);
-}
 
 template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
 __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
@@ -438,7 +387,6 @@ __global__ __launch_bounds__(256) void gemm_small_k4_kernel(int M, int N, int K,
 typedef __bf16 tbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 tbf16x2 __attribute__((ext_vector_type(2)));
 typedef float tfloatx2 __attribute__((ext_vector_type(2)));
-constexpr long long kSplitCounters = 256;  // int counters at the end of the split workspace (tiles64 < 256)
 constexpr int kX3BM = 128, kX3BN = 128, kX3BK = 32;
 constexpr int kX3RS = 40;                       // bf16 per LDS row (32 k + 8 pad = 80 B)
 constexpr int kX3Plane = 128 * kX3RS;           // bf16 per plane
@@ -719,24 +667,8 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     const long long MN = (long long)M * N;
     hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
                        ldb, C, ldc, epi, bias, H, Z, act);
-  } else if (split != nullptr && tiles64 < 256 && K >= 64 && 4ll * M * N <= split_cap - kSplitCounters) {
+  } else if (split != nullptr && tiles64 < 256 && K >= 64 && 4ll * M * N <= split_cap) {
     const dim3 grid((N + 63) / 64, (M + 63) / 64, 4);
-    static const bool fused = [] {
-      const char* e = std::getenv("ZF_TRAIN_FUSED_COMBINE");
-      return e && e[0] == '1';
-    }();
-    if (fused) {
-      // the last kSplitCounters ints of the split workspace: one zeroed counter per tile
-      int* cnt = reinterpret_cast<int*>(split + split_cap - kSplitCounters);
-      if (!tb)
-        hipLaunchKernelGGL((mgemm_splitq_fused_kernel<false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, split, cnt,
-                           C, ldc, epi, bias, H, Z, act);
-      else
-        hipLaunchKernelGGL((mgemm_splitq_fused_kernel<true>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, split, cnt,
-                           C, ldc, epi, bias, H, Z, act);
-      ZF_CHECK_LAUNCH("mgemm_splitq_fused_kernel");
-      return ZF_OK;
-    }
     if (!tb)
       hipLaunchKernelGGL((mgemm_kernel<64, 64, false, false, false, true>), grid, dim3(256), 0, st, M, N, K, A, lda, B,
                          ldb, split, N, kEpiNone, nullptr, nullptr, nullptr, 0, act);
@@ -758,8 +690,7 @@ inline unsigned blocks_for(long long n, int t = 256) { return (unsigned)((n + t 
 
 // Split-K workspace (floats) shared by the batch reductions below.
 constexpr int64_t kWsFloats = 32ll << 20;
-// The split-set GEMMs' partials (4 M N floats, M N < 256 tiles of 64 x 64),
-// the last kSplitCounters of them the fused combine's per-tile counters.
+// The split-set GEMMs' partials (4 M N floats, M N < 256 tiles of 64 x 64).
 constexpr int64_t kSplitFloats = 4ll << 20;
 
 // ---- batch reductions: row leaves + one fixed pairwise tree ----------------
@@ -2006,9 +1937,6 @@ int zf_trainer_create(const zf_flow_desc* desc_in, const float* blob_host, int64
   }
   t->d_ws = zf::dmalloc(t, zf::kWsFloats, rc);
   t->d_split = zf::dmalloc(t, zf::kSplitFloats, rc);
-  // the fused split-set combine's per-tile counters start at zero (each launch's last block resets its own)
-  if (!rc && hipMemset(t->d_split + zf::kSplitFloats - zf::kSplitCounters, 0, zf::kSplitCounters * sizeof(int)) != hipSuccess)
-    rc = zf::einval("zf_trainer: counter init failed");
   t->d_c = zf::dmalloc(t, B * (desc.cond_dim > 0 ? desc.cond_dim : 1), rc);
   t->d_bc = zf::dmalloc(t, 4, rc);
   {
