@@ -39,7 +39,7 @@ for _ in range(5):
 L.synchronize()
 t = buf.numpy().reshape(nwaves, 16).astype(np.float64)
 names = ["start->nsc", "layer0", "hidden", "hid->last", "last", "spline", "epilogue", "barrier_wait", "total",
-         "couplings", "sb"]
+         "couplings", "sb", "plain_step_dma_issue", "plain_step_group"]
 ncoup = t[:, 9].mean()
 res = {"config": name, "rows": N, "kernel": prog.kernel_variant, "couplings": ncoup}
 for k, nm in enumerate(names):

@@ -556,6 +556,8 @@ struct X3Pipe {
   int par_pieces;
 #ifdef ZF_X3_TRACE
   unsigned long long tbar;  // ticks spent in the per-group DMA wait + barrier
+  unsigned long long tdma;  // x3_step (plain steps: the dim-pair / hidden-256 last layers): DMA issue
+  unsigned long long tgrp;  // x3_step: the group's MFMAs, fragment reads and split (x3_group) + finish
 #endif
 };
 
@@ -603,7 +605,14 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
 #ifdef ZF_X3_TRACE
   p.tbar += X3T_NOW() - tb0;
 #endif
+#ifdef ZF_X3_TRACE
+  const unsigned long long td0 = X3T_NOW();
+#endif
   x3_issue_next<NT, T>(x3, p, p.nxt, lane);
+#ifdef ZF_X3_TRACE
+  const unsigned long long td1 = X3T_NOW();
+  p.tdma += td1 - td0;
+#endif
   if (bias != nullptr) {
     floatx16 bt[NOUT];
 #pragma unroll
@@ -614,6 +623,13 @@ __device__ __forceinline__ void x3_step(const char* __restrict__ x3, X3Pipe& p, 
   } else {
     x3_group<NT, T, NOUT, Q>(p.cur, hb, acc, lane);
   }
+#ifdef ZF_X3_TRACE
+  {  // wait for the group's MFMA results (a stamp cannot see an MFMA in flight)
+    float sink = acc[0][0];
+    asm volatile("; use %0" : "+v"(sink));
+    p.tgrp += X3T_NOW() - td1;
+  }
+#endif
   // SW: the layer input arrives as pre-activations except tile 0; the swish
   // of tile Q+1 goes here, in the same scheduling region as this group's
   // MFMAs, whose issue gaps it fills.
@@ -1483,6 +1499,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
   // 2 and 4), 8 total, 9 couplings, 10 other ops
   unsigned long long tacc[kX3TraceSlots] = {};
   pipe.tbar = 0;
+  pipe.tdma = 0;
+  pipe.tgrp = 0;
   const unsigned long long t_begin = X3T_NOW();
   unsigned long long t_last = t_begin;
 #define X3T(k)                                   \
@@ -1889,6 +1907,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #ifdef ZF_X3_TRACE
   X3T(6);
   tacc[7] = pipe.tbar;
+  tacc[11] = pipe.tdma;
+  tacc[12] = pipe.tgrp;
   tacc[8] = t_last - t_begin;
   if (lane == 0 && x3_trace_buf != nullptr) {
     unsigned long long* o = x3_trace_buf + ((long long)blockIdx.x * NW + wave) * kX3TraceSlots;
