@@ -81,8 +81,12 @@ CONFIGS = {
     "h512": dict(D=4, C=0, K=16, layers=(512, 512), latent="normal"),
     "h384c2": dict(D=3, C=2, K=8, layers=(384,), latent="beta", act="gelu"),
     "h1024k5": dict(D=5, C=0, K=5, layers=(1024, 64), latent="truncated_normal", couplings=2),
+    # a 260-wide input (K % 8 != 0) keeps Dense_1 on the trainer's GEMM, whose
+    # output row maxima then come from the standalone row-max kernel for the
+    # f16x2 last layer (zf_layered.hip)
+    "h260": dict(D=3, C=0, K=8, layers=(260, 264), latent="normal"),
 }
-LAYERED = ["h512", "h384c2", "h1024k5"]
+LAYERED = ["h512", "h384c2", "h1024k5", "h260"]
 ACTS = ["relu", "gelu", "tanh", "softplus", "sigmoid", "elu", "leaky_relu", "mixed", "mixed_fp32"]
 
 

@@ -47,9 +47,10 @@ inline int enotsup(const char* msg) {
 // Trainer pieces the layered eval path (zf_layered.hip) runs (zf_train.hip):
 // C = A . W + bias (W row-major [K][N], a FLAX Dense kernel) and, when H is
 // given, H = act(C) (the trainer's fused epilogue).  Mg: the batch that
-// picks the tile shape.
+// picks the tile shape.  rmax (optional): max |output row| as float bits
+// per row (H when given, else C) for a following f16x2 layer (zf_layered.hip).
 int dense_gemm(long long Mg, int M, int N, int K, const float* A, int lda, const float* W, int ldw, float* C,
-               int ldc, float* H, hipStream_t st, const float* bias, int act);
+               int ldc, float* H, hipStream_t st, const float* bias, int act, unsigned* rmax = nullptr);
 // One coupling's RQ spline over B rows from raw conditioner outputs P
 // [B][dt][3K-1] (normalize_spline_params + forward with log_det += into ld,
 // or inverse), state columns rotated by rot.

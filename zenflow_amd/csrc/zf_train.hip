@@ -320,20 +320,24 @@ __global__ void gemm_small_k_kernel(int M, int N, int K, const float* __restrict
 constexpr int kSk4Rows = 8;
 __global__ __launch_bounds__(256) void gemm_small_k4_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                      const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc, int epi,
-                                     const float* __restrict__ bias, float* __restrict__ H, int act) {
+                                     const float* __restrict__ bias, float* __restrict__ H, int act,
+                                     unsigned* __restrict__ rmax) {
   const int m0 = (blockIdx.y * 4 + threadIdx.y) * kSk4Rows;
   const int n = 4 * (blockIdx.x * 64 + threadIdx.x);
-  if (m0 >= M || n >= N) return;
+  if (m0 >= M) return;  // uniform per wave (a wave is one threadIdx.y)
+  const bool nok = n < N;
+  if (!nok && !rmax) return;
   float b[8][4], bs[4];
 #pragma unroll
   for (int k = 0; k < 8; ++k)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) b[k][t] = k < K ? B[(long long)k * ldb + n + t] : 0.f;
+    for (int t = 0; t < 4; ++t) b[k][t] = nok && k < K ? B[(long long)k * ldb + n + t] : 0.f;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) bs[t] = epi == kEpiBias ? bias[n + t] : 0.f;
+  for (int t = 0; t < 4; ++t) bs[t] = nok && epi == kEpiBias ? bias[n + t] : 0.f;
   for (int r = 0; r < kSk4Rows; ++r) {
     const int m = m0 + r;
     if (m >= M) break;
+    // (a lane past the last column, kept for the row max, multiplies zeros and stores nothing)
     float a[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] = k < K ? A[(long long)m * lda + k] : 0.f;
@@ -351,13 +355,23 @@ __global__ __launch_bounds__(256) void gemm_small_k4_kernel(int M, int N, int K,
       out[t] = v;
     }
     const long long o = (long long)m * ldc + n;
+    float mx = 0.f;
     if (epi == kEpiBias && H) {
       float y[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) y[t] = act == ZF_ACT_SWISH ? out[t] * sigmoidf(out[t]) : act_other(act, out[t]);
-      *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+      if (nok) *reinterpret_cast<float4*>(H + o) = float4{y[0], y[1], y[2], y[3]};
+      if (rmax && nok) mx = fmaxf(fmaxf(fabsf(y[0]), fabsf(y[1])), fmaxf(fabsf(y[2]), fabsf(y[3])));
+    } else if (rmax && nok) {
+      mx = fmaxf(fmaxf(fabsf(out[0]), fabsf(out[1])), fmaxf(fabsf(out[2]), fabsf(out[3])));
     }
-    if (C) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
+    if (C && nok) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
+    if (rmax) {
+      // max |row piece| over the wave's 256 columns, one atomic per row and wave
+#pragma unroll
+      for (int w = 1; w < 64; w <<= 1) mx = fmaxf(mx, __shfl_xor(mx, w));
+      if (threadIdx.x == 0) atomicMax(rmax + m, __float_as_uint(mx));
+    }
   }
 }
 
@@ -411,6 +425,18 @@ __device__ __forceinline__ void split3_store(const float (&x)[8], __bf16* p) {
   *reinterpret_cast<tbf16x8*>(p + 2 * kX3Plane) = l;
 }
 
+// The output tile of a persistent block's ti-th round.  Blocks go to the 8
+// XCDs round-robin (block b -> XCD b % 8), each XCD with its own L2; when
+// every round is full (gridDim % 8 == 0, ntiles % gridDim == 0) a round's
+// tiles are dealt in runs of gridDim / 8 consecutive tiles per XCD, so the
+// N-tiles of one row band (the same A rows) share an L2 instead of fetching
+// the rows once per XCD.  Which block computes a tile changes nothing else.
+__device__ __forceinline__ int x3_tile(int ti, int ntiles) {
+  const int b = blockIdx.x, G = gridDim.x;
+  if ((G & 7) == 0 && ntiles % G == 0) return ti * G + (b & 7) * (G >> 3) + (b >> 3);
+  return b + ti * G;
+}
+
 template <bool TB, bool WIDE>
 __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb, float* __restrict__ C,
@@ -433,41 +459,48 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
     float4 ra[4], rb[4];
     float rbs[16];
   };
+  // Every load is unconditional, from a clamped address, and nothing is
+  // computed from a loaded value until its stage is stored: a select right
+  // after a load (`ok ? x : 0`) makes the compiler wait for vmcnt(0) there,
+  // for the prefetch too.  Rows past M / columns past N read the last one
+  // (their outputs are not stored); k past K are zeroed when stored.
   // row-major [rows][K] tiles (A; B when TB): thread -> row e >> 2 (e = tid,
   // tid + 256), 8 consecutive k at 8 (e & 3) as two float4s
   auto load_rows = [&](const float* P, int ld, int r0, int R, int k0, float4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int e = tid + 256 * i, row = r0 + (e >> 2);
-      const float* src = P + (long long)row * ld + k0 + 8 * (e & 3);
-      const bool ok = row < R && k0 + 8 * (e & 3) < K;
-      v[2 * i] = ok ? *reinterpret_cast<const float4*>(src) : float4{0.f, 0.f, 0.f, 0.f};
-      v[2 * i + 1] = ok ? *reinterpret_cast<const float4*>(src + 4) : float4{0.f, 0.f, 0.f, 0.f};
+      const int e = tid + 256 * i, row = min(r0 + (e >> 2), R - 1);
+      const float* src = P + (long long)row * ld + min(k0 + 8 * (e & 3), K - 8);
+      v[2 * i] = *reinterpret_cast<const float4*>(src);
+      v[2 * i + 1] = *reinterpret_cast<const float4*>(src + 4);
     }
   };
-  auto store_rows = [&](__bf16* P, const float4 (&v)[4]) {
+  auto store_rows = [&](__bf16* P, const float4 (&v)[4], int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + 256 * i;
-      const float x[8] = {v[2 * i].x, v[2 * i].y, v[2 * i].z, v[2 * i].w,
-                          v[2 * i + 1].x, v[2 * i + 1].y, v[2 * i + 1].z, v[2 * i + 1].w};
+      const bool kok = k0 + 8 * (e & 3) < K;
+      const float4 u = kok ? v[2 * i] : float4{0.f, 0.f, 0.f, 0.f};
+      const float4 w = kok ? v[2 * i + 1] : float4{0.f, 0.f, 0.f, 0.f};
+      const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
       split3_store(x, P + (e >> 2) * kX3RS + 8 * (e & 3));
     }
   };
   // B row-major [K][N] (!TB): thread -> column n0 + (tid & 127), k 16 (tid >> 7) .. +15
   auto load_cols = [&](int tn0, int k0, float (&v)[16]) {
-    const int n = tn0 + (tid & 127);
+    const int n = min(tn0 + (tid & 127), N - 1);
     const int kb = k0 + 16 * (tid >> 7);
-    const float* src = B + (long long)kb * ldb + n;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = n < N && kb + j < K ? src[(long long)j * ldb] : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = B[(long long)min(kb + j, K - 1) * ldb + n];
   };
-  auto store_cols = [&](const float (&v)[16]) {
+  auto store_cols = [&](const float (&v)[16], int k0) {
     __bf16* P = Bp + (tid & 127) * kX3RS + 16 * (tid >> 7);
+    const int kb = k0 + 16 * (tid >> 7);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const float x[8] = {v[8 * g], v[8 * g + 1], v[8 * g + 2], v[8 * g + 3],
-                          v[8 * g + 4], v[8 * g + 5], v[8 * g + 6], v[8 * g + 7]};
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = kb + 8 * g + u < K ? v[8 * g + u] : 0.f;
       split3_store(x, P + 8 * g);
     }
   };
@@ -483,15 +516,21 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
   const int total = mine * kt;
   auto load = [&](int it, Stage& st) __attribute__((always_inline)) {
     const int ti = it / kt, k0 = (it - ti * kt) * kX3BK;
-    const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+    const int tile = x3_tile(ti, ntiles);
     const int tm0 = (tile / tiles_n) * kX3BM, tn0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
     load_rows(A, lda, tm0, M, k0, st.ra);
     if (TB) load_rows(B, ldb, tn0, N, k0, st.rb);
     else load_cols(tn0, k0, st.rbs);
   };
+  if (total == 0) return;
+  // Straight-line staging (gemm_h2_kernel, zf_layered.hip): both stages
+  // loaded before the loop, two k-steps per iteration with unconditional
+  // refills, an odd last k-step after it — a skipped refill on any path
+  // leaves the compiler unsure which stage is newest, and it then waits for
+  // every load at each stage store (Dense 512 x 512 eval: 1.4x faster).
   Stage S0, S1;
-  if (total > 0) load(0, S0);
-  if (total > 1) load(1, S1);
+  load(0, S0);
+  load(min(1, total - 1), S1);
   floatx16 acc[2][2];
   auto epilogue = [&]() __attribute__((always_inline)) {
     if (WIDE) {
@@ -537,7 +576,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
   auto kstep = [&](int it, Stage& S) __attribute__((always_inline)) {
     const int ti = it / kt, kk = it - ti * kt;
     if (kk == 0) {
-      const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
+      const int tile = x3_tile(ti, ntiles);
       m0 = (tile / tiles_n) * kX3BM;
       n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
 #pragma unroll
@@ -545,11 +584,11 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
     }
-    store_rows(Ap, S.ra);
-    if (TB) store_rows(Bp, S.rb);
-    else store_cols(S.rbs);
+    store_rows(Ap, S.ra, kk * kX3BK);
+    if (TB) store_rows(Bp, S.rb, kk * kX3BK);
+    else store_cols(S.rbs, kk * kX3BK);
     __syncthreads();
-    if (it + 2 < total) load(it + 2, S);
+    load(min(it + 2, total - 1), S);  // (the last two refills repeat a k-tile, unused)
 #pragma unroll
     for (int s = 0; s < kX3BK / 16; ++s) {
       tbf16x8 af[2][3], bf[2][3];
@@ -582,10 +621,24 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
     __syncthreads();
     if (kk == kt - 1) epilogue();
   };
-  for (int it = 0; it < total; it += 2) {
+  int it = 0;
+  for (; it + 1 < total; it += 2) {
     kstep(it, S0);
-    if (it + 1 < total) kstep(it + 1, S1);
+    kstep(it + 1, S1);
   }
+  if (it < total) kstep(it, S0);
+}
+
+// max |H[m][0..N)| as float bits into r[m] (a producer without the fused row max)
+__global__ __launch_bounds__(256) void row_absmax_kernel(int M, int N, const float* __restrict__ H, int ldh,
+                                                         unsigned* __restrict__ r) {
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (m >= M) return;
+  float mx = 0.f;
+  for (int n = lane; n < N; n += 64) mx = fmaxf(mx, fabsf(H[(long long)m * ldh + n]));
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) mx = fmaxf(mx, __shfl_xor(mx, w));
+  if (lane == 0) r[m] = __float_as_uint(mx);
 }
 
 template <int T>
@@ -611,7 +664,8 @@ void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const fl
 // per output (gemm_small_k_kernel; same bits); ZF_TRAIN_SPLITQ=0: neither.
 int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
          int ldc, hipStream_t st, int epi = kEpiNone, const float* bias = nullptr, float* H = nullptr,
-         const float* Z = nullptr, int act = ZF_ACT_SWISH, float* split = nullptr, long long split_cap = 0) {
+         const float* Z = nullptr, int act = ZF_ACT_SWISH, float* split = nullptr, long long split_cap = 0,
+         unsigned* rmax = nullptr, bool* rmax_done = nullptr) {
   if (M <= 0 || N <= 0) return ZF_OK;
   const long long big = (long long)((N + 127) / 128) * ((Mg + 127) / 128);
   const long long tiles64 = (long long)((N + 63) / 64) * ((M + 63) / 64);
@@ -630,8 +684,9 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     if (N % 4 == 0 && ldc % 4 == 0 && al16(C) && al16(H) && (epi == kEpiBias || epi == kEpiNone)) {
       hipLaunchKernelGGL(gemm_small_k4_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)((M + 4 * kSk4Rows - 1) / (4 * kSk4Rows))),
-                         dim3(64, 4), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, H, act);
+                         dim3(64, 4), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, H, act, rmax);
       ZF_CHECK_LAUNCH("gemm_small_k4_kernel");
+      if (rmax_done) *rmax_done = rmax != nullptr;
       return ZF_OK;
     }
     hipLaunchKernelGGL(gemm_small_k_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, st, M, N, K, A, lda, B,
@@ -2406,8 +2461,15 @@ int zf_trainer_set_blob(zf_trainer_t* t, const float* blob_host) {
 namespace zf {
 
 int dense_gemm(long long Mg, int M, int N, int K, const float* A, int lda, const float* W, int ldw, float* C,
-               int ldc, float* H, hipStream_t st, const float* bias, int act) {
-  return gemm(false, Mg, M, N, K, A, lda, W, ldw, C, ldc, st, bias ? kEpiBias : kEpiNone, bias, H, nullptr, act);
+               int ldc, float* H, hipStream_t st, const float* bias, int act, unsigned* rmax) {
+  if (rmax && M > 0) ZF_TRY_HIP(hipMemsetAsync(rmax, 0, (size_t)M * sizeof(unsigned), st));
+  bool done = false;
+  const int rc = gemm(false, Mg, M, N, K, A, lda, W, ldw, C, ldc, st, bias ? kEpiBias : kEpiNone, bias, H, nullptr,
+                      act, nullptr, 0, rmax, &done);
+  if (rc || !rmax || done || M <= 0) return rc;
+  hipLaunchKernelGGL(row_absmax_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, M, N, H ? H : C, ldc, rmax);
+  ZF_CHECK_LAUNCH("row_absmax_kernel");
+  return ZF_OK;
 }
 
 int spline_rows(bool inverse, const float* s_in, float* s_out, const float* P, float* ld, int B, int D, int dt,
