@@ -7,9 +7,12 @@
 // Op by op over chunks of rows, every intermediate in HBM:
 //   ShiftBounds        lay_sb_kernel       (zf_flow_dev.h sb_*_elem, the fused kernels' math)
 //   NSC conditioner    lay_bn_kernel       hstack(xc, c) -> BatchNorm (eval: running stats)
-//                      dense_gemm          Dense_l + activation: the trainer's GEMMs
-//                                          (bf16x3 split MFMA at >= 512 128x128 tiles, else fp32 MFMA)
-//                      dense_gemm          last Dense -> raw spline parameters P [rows][dt][3K-1]
+//                      dense_gemm          Dense_0 + activation: the trainer's GEMMs (K <= 8: one
+//                                          thread per 4 outputs), leaving the row maxima of its output
+//                      dense_gemm_h2       Dense_l (l >= 1) + activation on f16x2 split MFMA with
+//                                          per-row scales (gemm_h2_kernel below; K % 8 != 0 or
+//                                          ZF_LAYERED_H2=0: the trainer's bf16x3 / fp32 GEMMs)
+//                      dense_gemm_h2       last Dense -> raw spline parameters P [rows][dt][3K-1]
 //   NSC spline         spline_rows         normalize_spline_params + RQ forward (log_det) / inverse
 //   Roll               a rotation of the column index, no data movement
 //   latent             lay_latent_kernel   log_prob + nan_to_num + the 128-row NLL partials
@@ -140,7 +143,21 @@ __global__ void lay_draw_kernel(float* __restrict__ s, int B, long long row0, in
 // gemm_x3_kernel's tile geometry (zf_train.hip) and its XCD-aware tile order
 constexpr int kX3BM = 128, kX3BN = 128, kX3BK = 32;
 constexpr int kX3RS = 40;              // halfs per LDS row (32 k + 8 pad = 80 B)
-constexpr int kX3Plane = 128 * kX3RS;  // halfs per plane
+// gemm_h2_kernel's LDS: ZF_H2_DB (default) double-buffers the k-tile stage
+// (one barrier per k-tile instead of two) in 64-B rows whose 16-B chunks are
+// XOR-swizzled by row bits 2-3 (16 lanes of a fragment read or a stage store
+// hit 16 distinct 4-bank groups; the 80-B padded rows of one buffer would
+// not leave room for two blocks per CU)
+#ifndef ZF_H2_DB
+#define ZF_H2_DB 1
+#endif
+constexpr bool kH2DB = ZF_H2_DB != 0;
+constexpr int kH2RS = kH2DB ? 32 : kX3RS;  // halfs per LDS row
+constexpr int kH2Pl = 128 * kH2RS;         // halfs per plane
+constexpr int kH2Buf = 4 * kH2Pl;          // one stage: A hi, A lo, B hi, B lo
+__device__ __forceinline__ int h2_off(int row, int chunk) {
+  return kH2DB ? row * 32 + 8 * (chunk ^ ((row >> 2) & 3)) : row * kX3RS + 8 * chunk;
+}
 typedef float tfloatx2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
@@ -188,24 +205,26 @@ __device__ __forceinline__ void split2_store(const float (&x)[8], int sh, _Float
     lv[2 * i] = vl[0]; lv[2 * i + 1] = vl[1];
   }
   *reinterpret_cast<thalf8*>(p) = hv;
-  *reinterpret_cast<thalf8*>(p + kX3Plane) = lv;
+  *reinterpret_cast<thalf8*>(p + kH2Pl) = lv;
 }
 
+// The epilogue's activation.  SW: swish only — the act switch of every other
+// activation, unrolled over the epilogue's 16 row pieces, made the kernel
+// ~300 KB of code, fetched cold at every tile's epilogue.
+template <bool SW>
 __device__ __forceinline__ float h2_act(int act, float v) {
-  return act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
+  return SW || act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
 }
 
-template <bool WIDE>
+template <bool WIDE, bool SW>
 __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                       const _Float16* __restrict__ Wp, const unsigned* __restrict__ rin,
                                                       int kw, float* __restrict__ C, int ldc,
                                                       const float* __restrict__ bias, float* __restrict__ H,
                                                       unsigned* __restrict__ rout, int act) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds[4 * kX3Plane];
+  __shared__ __attribute__((aligned(16))) _Float16 lds[(kH2DB ? 2 : 1) * kH2Buf];
   __shared__ unsigned rowx[kX3BM];  // the tile's A-row maxima (float bits)
   __shared__ __attribute__((aligned(16))) float biasl[kX3BN];    // the tile's bias
-  _Float16* const Ap = lds;
-  _Float16* const Bp = lds + 2 * kX3Plane;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 64;
@@ -224,7 +243,10 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
   };
   const int tiles_n = (N + kX3BN - 1) / kX3BN;
   const int ntiles = tiles_n * ((M + kX3BM - 1) / kX3BM);
-  const int kt = (K + kX3BK - 1) / kX3BK;
+  // k-tiles per output tile, rounded up to even (pack_w_h2 zero-fills the
+  // extra W block; its A k are past K and zeroed): the tile loop below runs
+  // them as (S0, S1) pairs, so the epilogue is emitted once
+  const int kt = ((K + kX3BK - 1) / kX3BK + 1) & ~1;
   const int mine = ntiles > (int)blockIdx.x ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
   const int total = mine * kt;
   // A: thread -> rows (e >> 2) for e = tid, tid + 256, 8 k at 8 (e & 3) (rows past M
@@ -248,12 +270,12 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
     for (int q = 0; q < 4; ++q) st.rb[q] = wsrc[tid + 256 * q];
   };
   if (total == 0) return;
-  // Straight-line staging: both stages loaded before the loop, the loop body
-  // two k-steps (S0 then S1) with the refill unconditional, an odd last
-  // k-step after it.  Any path that skips a refill (an `if` around a load
-  // or around the second k-step) leaves the compiler's wait counting unsure
-  // which stage is newest, and it then waits for all loads (vmcnt(0)) at
-  // every stage store: a one-deep prefetch.
+  // Straight-line staging: both stages loaded before the loop, the k-loop
+  // body two k-steps (S0 then S1) with the refill unconditional.  Any path
+  // that skips a refill (an `if` around a load or around the second k-step)
+  // leaves the compiler's wait counting unsure which stage is newest, and it
+  // then waits for all loads (vmcnt(0)) at every stage store: a one-deep
+  // prefetch.
   Stage S0, S1;
   load(0, S0);
   load(min(1, total - 1), S1);
@@ -286,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
             if (C) *reinterpret_cast<float4*>(C + o) = float4{x[0], x[1], x[2], x[3]};
             if (H) {
 #pragma unroll
-              for (int u = 0; u < 4; ++u) x[u] = h2_act(act, x[u]);
+              for (int u = 0; u < 4; ++u) x[u] = h2_act<SW>(act, x[u]);
               *reinterpret_cast<float4*>(H + o) = float4{x[0], x[1], x[2], x[3]};
             }
             mx = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
@@ -316,24 +338,17 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
             float v = ldexpf(acc[i][j][q], us) + biasl[wn0 + 32 * j + r];
             const long long o = (long long)m * ldc + n;
             if (C) C[o] = v;
-            if (H) H[o] = v = h2_act(act, v);
+            if (H) H[o] = v = h2_act<SW>(act, v);
             if (rout) atomicMax(rout + m, __float_as_uint(fabsf(v)));
           }
         }
     }
     __syncthreads();
   };
-  auto kstep = [&](int it, Stage& S) __attribute__((always_inline)) {
-    const int ti = it / kt, kk = it - ti * kt, k0 = kk * kX3BK;
-    if (kk == 0) {
-      const int tile = x3_tile(ti, ntiles);
-      m0 = (tile / tiles_n) * kX3BM;
-      n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
-    }
+  auto kstep = [&](int it, int kk, Stage& S) __attribute__((always_inline)) {
+    const int k0 = kk * kX3BK;
+    _Float16* const Ap = lds + (kH2DB ? (it & 1) * kH2Buf : 0);  // this k-tile's stage buffer
+    _Float16* const Bp = Ap + 2 * kH2Pl;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + 256 * i;
@@ -341,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
       const float4 u = kok ? S.ra[2 * i] : float4{0.f, 0.f, 0.f, 0.f};
       const float4 w = kok ? S.ra[2 * i + 1] : float4{0.f, 0.f, 0.f, 0.f};
       const float x[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-      split2_store(x, 14 - h2_row_exp(S.rr[i]), Ap + (e >> 2) * kX3RS + 8 * (e & 3));
+      split2_store(x, 14 - h2_row_exp(S.rr[i]), Ap + h2_off(e >> 2, e & 3));
       if ((e & 3) == 0) rowx[e >> 2] = S.rr[i];  // (every k-tile of the tile: the same values)
     }
     if (tid < kX3BN) biasl[tid] = S.bs;
@@ -350,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
       // packed block [plane][n 0..127][k 0..31]: dwordx4 f = tid + 256 q -> plane f >> 9,
       // row (f >> 2) & 127, k 8 (f & 3)
       const int f = tid + 256 * q;
-      *reinterpret_cast<uint4*>(Bp + (f >> 9) * kX3Plane + ((f >> 2) & 127) * kX3RS + 8 * (f & 3)) = S.rb[q];
+      *reinterpret_cast<uint4*>(Bp + (f >> 9) * kH2Pl + h2_off((f >> 2) & 127, f & 3)) = S.rb[q];
     }
     __syncthreads();
     load(min(it + 2, total - 1), S);  // (the last two refills repeat a k-tile, unused)
@@ -361,8 +376,8 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          af[i][t] = *reinterpret_cast<const thalf8*>(Ap + t * kX3Plane + (wm0 + 32 * i + r) * kX3RS + 16 * s + 8 * h);
-          bf[i][t] = *reinterpret_cast<const thalf8*>(Bp + t * kX3Plane + (wn0 + 32 * i + r) * kX3RS + 16 * s + 8 * h);
+          af[i][t] = *reinterpret_cast<const thalf8*>(Ap + t * kH2Pl + h2_off(wm0 + 32 * i + r, 2 * s + h));
+          bf[i][t] = *reinterpret_cast<const thalf8*>(Bp + t * kH2Pl + h2_off(wn0 + 32 * i + r, 2 * s + h));
         }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -377,15 +392,27 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
           acc[i][j] = mf(0, 0, c);
         }
     }
-    __syncthreads();
-    if (kk == kt - 1) epilogue();
+    // single buffer: the next store overwrites this stage; double buffer: the
+    // next store goes to the other one, which every wave finished reading
+    // before passing this k-tile's barrier
+    if (!kH2DB) __syncthreads();
   };
   int it = 0;
-  for (; it + 1 < total; it += 2) {
-    kstep(it, S0);
-    kstep(it + 1, S1);
+  for (int ti = 0; ti < mine; ++ti) {
+    const int tile = x3_tile(ti, ntiles);
+    m0 = (tile / tiles_n) * kX3BM;
+    n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+    for (int kk = 0; kk < kt; kk += 2, it += 2) {
+      kstep(it, kk, S0);
+      kstep(it + 1, kk + 1, S1);
+    }
+    if (kH2DB) __syncthreads();  // the epilogue's LDS transpose spans both stage buffers
+    epilogue();
   }
-  if (it < total) kstep(it, S0);
 }
 
 int dense_gemm_h2(int M, int N, int K, const float* A, int lda, const void* Wp, const unsigned* rin, int kw,
@@ -401,12 +428,18 @@ int dense_gemm_h2(int M, int N, int K, const float* A, int lda, const void* Wp, 
   const dim3 grid((unsigned)std::min<long long>(ntiles, 2ll * ncu));
   const bool wide = N % 4 == 0 && ldc % 4 == 0 && (!C || al16(C)) && (!H || al16(H));
   const _Float16* W = static_cast<const _Float16*>(Wp);
-  if (wide)
-    hipLaunchKernelGGL(gemm_h2_kernel<true>, grid, dim3(256), 0, st, M, N, K, A, lda, W, rin, kw, C, ldc, bias, H,
-                       rout, act);
-  else
-    hipLaunchKernelGGL(gemm_h2_kernel<false>, grid, dim3(256), 0, st, M, N, K, A, lda, W, rin, kw, C, ldc, bias, H,
-                       rout, act);
+  const bool sw = act == ZF_ACT_SWISH || !H;  // no activation stored: the swish-only form
+#define ZF_H2_LAUNCH(W_, S_)                                                                                    \
+  hipLaunchKernelGGL((gemm_h2_kernel<W_, S_>), grid, dim3(256), 0, st, M, N, K, A, lda, W, rin, kw, C, ldc, bias, \
+                     H, rout, act)
+  if (wide) {
+    if (sw) ZF_H2_LAUNCH(true, true);
+    else ZF_H2_LAUNCH(true, false);
+  } else {
+    if (sw) ZF_H2_LAUNCH(false, true);
+    else ZF_H2_LAUNCH(false, false);
+  }
+#undef ZF_H2_LAUNCH
   ZF_CHECK_LAUNCH("gemm_h2_kernel");
   return ZF_OK;
 }
@@ -417,7 +450,7 @@ void pack_w_h2(const float* W, int K, int N, std::vector<uint16_t>& out, int& kw
   int e = 0;
   (void)std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
   kw = (mx > 0.f && std::isfinite(mx)) ? 14 - e : 0;
-  const int tn = (N + 127) / 128, tk = (K + kX3BK - 1) / kX3BK;
+  const int tn = (N + 127) / 128, tk = ((K + kX3BK - 1) / kX3BK + 1) & ~1;  // even (gemm_h2_kernel)
   out.assign((size_t)tn * tk * kH2Tile, 0);
   for (int a = 0; a < tn; ++a)
     for (int b = 0; b < tk; ++b) {

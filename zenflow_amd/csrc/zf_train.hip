@@ -437,7 +437,7 @@ __device__ __forceinline__ int x3_tile(int ti, int ntiles) {
   return b + ti * G;
 }
 
-template <bool TB, bool WIDE>
+template <bool TB, bool WIDE, bool SW>
 __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                       const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                       int ldc, int epi, const float* __restrict__ bias,
@@ -511,7 +511,13 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
   // block) x kt k-tiles + k-tile kk.
   const int tiles_n = (N + kX3BN - 1) / kX3BN;
   const int ntiles = tiles_n * ((M + kX3BM - 1) / kX3BM);
-  const int kt = (K + kX3BK - 1) / kX3BK;
+  // k-tiles per output tile, rounded up to even (an odd K / 32's extra
+  // k-tile is past K: zeroed when stored) so the tile loop below runs them
+  // as (S0, S1) pairs and the epilogue is emitted once (three inlined
+  // copies of the generic epilogue made the kernel too big for the
+  // instruction cache; SW, swish couplings, leaves out the other
+  // activations' code)
+  const int kt = ((K + kX3BK - 1) / kX3BK + 1) & ~1;
   const int mine = ntiles > (int)blockIdx.x ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
   const int total = mine * kt;
   auto load = [&](int it, Stage& st) __attribute__((always_inline)) {
@@ -554,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
           const int row = 4 * t + (lane >> 4), c4 = lane & 15;
           const float4 v = *reinterpret_cast<const float4*>(T + row * 68 + 4 * c4);
           const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 4 * c4;
-          if (m < M && n < N) gemm_epilogue4(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+          if (m < M && n < N) gemm_epilogue4(v, n, (long long)m * ldc + n, C, epi, bias, H, Z, SW ? ZF_ACT_SWISH : act);
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
@@ -567,23 +573,14 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
   #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-            if (m < M && n < N) gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+            if (m < M && n < N)
+              gemm_epilogue(acc[i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, SW ? ZF_ACT_SWISH : act);
           }
     }
     __syncthreads();  // the next tile's planes overwrite the epilogue's LDS
   };
   // one k-iteration from stage S (refilled with iteration it + 2 once stored)
-  auto kstep = [&](int it, Stage& S) __attribute__((always_inline)) {
-    const int ti = it / kt, kk = it - ti * kt;
-    if (kk == 0) {
-      const int tile = x3_tile(ti, ntiles);
-      m0 = (tile / tiles_n) * kX3BM;
-      n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
-    }
+  auto kstep = [&](int it, int kk, Stage& S) __attribute__((always_inline)) {
     store_rows(Ap, S.ra, kk * kX3BK);
     if (TB) store_rows(Bp, S.rb, kk * kX3BK);
     else store_cols(S.rbs, kk * kX3BK);
@@ -619,14 +616,22 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(int M, int N, int K, co
         }
     }
     __syncthreads();
-    if (kk == kt - 1) epilogue();
   };
   int it = 0;
-  for (; it + 1 < total; it += 2) {
-    kstep(it, S0);
-    kstep(it + 1, S1);
+  for (int ti = 0; ti < mine; ++ti) {
+    const int tile = x3_tile(ti, ntiles);
+    m0 = (tile / tiles_n) * kX3BM;
+    n0 = (tile - (tile / tiles_n) * tiles_n) * kX3BN;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+    for (int kk = 0; kk < kt; kk += 2, it += 2) {
+      kstep(it, kk, S0);
+      kstep(it + 1, kk + 1, S1);
+    }
+    epilogue();
   }
-  if (it < total) kstep(it, S0);
 }
 
 // max |H[m][0..N)| as float bits into r[m] (a producer without the fused row max)
@@ -702,16 +707,21 @@ int gemm(bool tb, long long Mg, int M, int N, int K, const float* A, int lda, co
     const dim3 grid((unsigned)std::min<long long>(ntiles, 2ll * ncu));
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool wide = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!H || al16(H)) && (!Z || al16(Z));
-#define ZF_X3_LAUNCH(TB_, W_)                                                                                    \
-  hipLaunchKernelGGL((gemm_x3_kernel<TB_, W_>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, \
-                     H, Z, act)
+    // the swish-only epilogue whenever no other activation is applied
+    const bool sw = act == ZF_ACT_SWISH || epi == kEpiNone || (epi == kEpiBias && !H);
+#define ZF_X3_LAUNCH(TB_, W_, S_)                                                                                    \
+  hipLaunchKernelGGL((gemm_x3_kernel<TB_, W_, S_>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, epi, \
+                     bias, H, Z, act)
+#define ZF_X3_LAUNCH_SW(TB_, W_) \
+  if (sw) ZF_X3_LAUNCH(TB_, W_, true); else ZF_X3_LAUNCH(TB_, W_, false)
     if (tb) {
-      if (wide) ZF_X3_LAUNCH(true, true);
-      else ZF_X3_LAUNCH(true, false);
+      if (wide) ZF_X3_LAUNCH_SW(true, true);
+      else ZF_X3_LAUNCH_SW(true, false);
     } else {
-      if (wide) ZF_X3_LAUNCH(false, true);
-      else ZF_X3_LAUNCH(false, false);
+      if (wide) ZF_X3_LAUNCH_SW(false, true);
+      else ZF_X3_LAUNCH_SW(false, false);
     }
+#undef ZF_X3_LAUNCH_SW
 #undef ZF_X3_LAUNCH
     ZF_CHECK_LAUNCH("gemm_x3_kernel");
     return ZF_OK;
