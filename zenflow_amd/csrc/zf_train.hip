@@ -117,7 +117,10 @@ __device__ __forceinline__ void gemm_epilogue4(float4 v, int n, long long o, flo
 // blocks (small batches: 1024 rows give 32 tiles for 256 CUs).
 // The block body, with the block's coordinates passed in (mgemm_kernel: its
 // blockIdx; wgrad_group_kernel: decoded from one launch over several GEMMs).
-template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ>
+// SW: no activation but swish in the epilogue (its code only; the generic
+// form's act switch made the 128 x 128 kernel ~255 KB, fetched cold at
+// every epilogue)
+template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ, bool SW = false>
 __device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K, const float* __restrict__ A, int lda,
                                            const float* __restrict__ B, int ldb, float* __restrict__ C, int ldc,
                                            int epi, const float* __restrict__ bias, float* __restrict__ H,
@@ -259,18 +262,20 @@ __device__ __forceinline__ void mgemm_body(const uint3 bid, int M, int N, int K,
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = m0 + wm0 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h, n = n0 + wn0 + 32 * j + r;
-        if (m < M && n < N) gemm_epilogue(acc[0][i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, act);
+        if (m < M && n < N)
+          gemm_epilogue(acc[0][i][j][q], n, (long long)m * ldc + n, C, epi, bias, H, Z, SW ? ZF_ACT_SWISH : act);
       }
 }
 
 
-template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false>
+template <int BM, int BN, bool TA, bool TB, bool WG, bool SPLITQ = false, bool SW = false>
 __global__ __launch_bounds__(256) void mgemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float* __restrict__ C,
                                                     int ldc, int epi, const float* __restrict__ bias,
                                                     float* __restrict__ H, const float* __restrict__ Z, int KC,
                                                     int act) {
-  mgemm_body<BM, BN, TA, TB, WG, SPLITQ>(uint3{blockIdx.x, blockIdx.y, blockIdx.z}, M, N, K, A, lda, B, ldb, C, ldc, epi, bias, H, Z, KC, act);
+  mgemm_body<BM, BN, TA, TB, WG, SPLITQ, SW>(uint3{blockIdx.x, blockIdx.y, blockIdx.z}, M, N, K, A, lda, B, ldb, C,
+                                             ldc, epi, bias, H, Z, KC, act);
 }
 
 __global__ void gemm_combine_kernel(int M, int N, const float* __restrict__ P, float* __restrict__ C, int ldc,
@@ -650,12 +655,18 @@ template <int T>
 void gemm_launch(bool tb, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
                  hipStream_t st, int epi, const float* bias, float* H, const float* Z, int act) {
   const dim3 grid((N + T - 1) / T, (M + T - 1) / T);
-  if (!tb)
-    hipLaunchKernelGGL((mgemm_kernel<T, T, false, false, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, bias, H, Z, 0, act);
-  else
-    hipLaunchKernelGGL((mgemm_kernel<T, T, false, true, false>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C,
-                       ldc, epi, bias, H, Z, 0, act);
+  const bool sw = act == ZF_ACT_SWISH || epi == kEpiNone || (epi == kEpiBias && !H);
+#define ZF_MG_LAUNCH(TB_, SW_)                                                                                \
+  hipLaunchKernelGGL((mgemm_kernel<T, T, false, TB_, false, false, SW_>), grid, dim3(256), 0, st, M, N, K, A, lda, \
+                     B, ldb, C, ldc, epi, bias, H, Z, 0, act)
+  if (!tb) {
+    if (sw) ZF_MG_LAUNCH(false, true);
+    else ZF_MG_LAUNCH(false, false);
+  } else {
+    if (sw) ZF_MG_LAUNCH(true, true);
+    else ZF_MG_LAUNCH(true, false);
+  }
+#undef ZF_MG_LAUNCH
 }
 
 // C = A . op(B) with A row-major [M][K]; 128 x 128 tiles when they give at
