@@ -392,6 +392,55 @@ def test_split_scaling_extremes(scheme, name, regime, monkeypatch):
     check_lp(gpu_log_prob(case), case, f"{scheme}/{name}/{regime}")
 
 
+@pytest.mark.parametrize("name", ["h512", "h384c2"])
+@pytest.mark.parametrize("regime", ["huge_activations", "tiny_activations", "tiny_weights", "huge_weights"])
+def test_layered_scaling_extremes(name, regime):
+    """The layered path's f16x2 GEMMs (zf_layered.hip gemm_h2_kernel) scale
+    each activation row by its producer's row maximum and each weight matrix
+    by its own: parity must not depend on the magnitudes (the fused kernels'
+    regimes above, on hidden widths > 256)."""
+    case = make_case(name, N=1500, seed=39)
+    params = case["variables"]["params"]["bijector"]
+    last = f"Dense_{len(case['cfg']['layers'])}"
+    for key, p in params.items():
+        if regime == "huge_activations":
+            p["BatchNorm_0"]["scale"] = (p["BatchNorm_0"]["scale"] * 3e3).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-3).astype(F32)
+        elif regime == "tiny_activations":
+            p["Dense_0"]["kernel"] = (p["Dense_0"]["kernel"] * 1e-6).astype(F32)
+            p["Dense_0"]["bias"] = (p["Dense_0"]["bias"] * 1e-6).astype(F32)
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e4).astype(F32)
+        elif regime == "tiny_weights":
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e-7).astype(F32)
+        else:
+            p["Dense_1"]["kernel"] = (p["Dense_1"]["kernel"] * 1e5).astype(F32)
+            if last != "Dense_1":
+                p[last]["kernel"] = (p[last]["kernel"] * 1e-5).astype(F32)
+            else:  # one hidden layer: the huge last layer reads tiny activations instead
+                p["Dense_0"]["kernel"] = (p["Dense_0"]["kernel"] * 1e-5).astype(F32)
+                p["Dense_0"]["bias"] = (p["Dense_0"]["bias"] * 1e-5).astype(F32)
+    _, bf = _bound(case)
+    assert bf.program.kernel_variant == "layered"
+    check_lp(gpu_log_prob(case), case, f"layered/{name}/{regime}")
+
+
+@pytest.mark.parametrize("name", ["h512", "h384c2"])
+def test_layered_nonfinite_rows(name):
+    """Rows with NaN, +-inf and 1e30 inputs next to ordinary rows: a row's
+    maximum (the f16x2 scale of its activations) must neither leak into other
+    rows nor turn a finite row non-finite; non-finite rows give the oracle's
+    flow.py:47 value."""
+    case = make_case(name, N=1000, seed=40)
+    x = case["x"].copy()
+    x[3, :] = np.nan
+    x[4, 0] = np.inf
+    x[5, -1] = -np.inf
+    x[6, :] = 1e30
+    x[7, 0] = -1e30
+    case = dict(case, x=x)
+    check_lp(gpu_log_prob(case), case, f"layered/{name}/nonfinite")
+
+
 @pytest.mark.parametrize("name", X3_ACTS)
 @pytest.mark.parametrize("regime", ["huge_activations", "tiny_activations", "tiny_weights", "huge_weights"])
 def test_split_scaling_extremes_other_acts(name, regime, monkeypatch):
