@@ -208,12 +208,30 @@ __device__ __forceinline__ void split2_store(const float (&x)[8], int sh, _Float
   *reinterpret_cast<thalf8*>(p + kH2Pl) = lv;
 }
 
+// max of x over each 16-lane DPP row (every lane of the row gets it)
+__device__ __forceinline__ float h2_max16(float x) {
+  auto step = [](float v, int ctrl) {
+    const int o = ctrl == 0xB1   ? __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)
+                  : ctrl == 0x4E ? __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)
+                  : ctrl == 0x141 ? __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)
+                                  : __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false);
+    return fmaxf(v, __int_as_float(o));
+  };
+  x = step(x, 0xB1);   // quad_perm [1, 0, 3, 2]
+  x = step(x, 0x4E);   // quad_perm [2, 3, 0, 1]
+  x = step(x, 0x141);  // row_half_mirror
+  return step(x, 0x140);  // row_mirror
+}
+
 // The epilogue's activation.  SW: swish only — the act switch of every other
 // activation, unrolled over the epilogue's 16 row pieces, made the kernel
 // ~300 KB of code, fetched cold at every tile's epilogue.
+// Swish with the hardware exp and reciprocal (~1 ulp each) instead of the
+// IEEE divide: ~8 fewer VALU per value, a third of the epilogue (its error,
+// a few 1e-7, is that of the f16x2 split the next layer applies anyway).
 template <bool SW>
 __device__ __forceinline__ float h2_act(int act, float v) {
-  return SW || act == ZF_ACT_SWISH ? v * sigmoidf(v) : act_other(act, v);
+  return SW || act == ZF_ACT_SWISH ? v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)) : act_other(act, v);
 }
 
 template <bool WIDE, bool SW>
@@ -314,9 +332,10 @@ __global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, co
             mx = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
           }
           if (rout) {
-            // the 16 lanes of one row piece (64 columns), then one atomic per row and wave
-#pragma unroll
-            for (int w = 1; w < 16; w <<= 1) mx = fmaxf(mx, __shfl_xor(mx, w));
+            // max over the 16 lanes of one row piece (64 columns) by DPP within
+            // the 16-lane row (quad xor 1, quad xor 2, half-row mirror, row
+            // mirror: four VALU, no LDS permute), then one atomic per row and wave
+            mx = h2_max16(mx);
             if (c4 == 0 && m < M) atomicMax(rout + m, __float_as_uint(mx));
           }
         }
