@@ -372,10 +372,19 @@ __global__ __launch_bounds__(256) void gemm_small_k4_kernel(int M, int N, int K,
     }
     if (C && nok) *reinterpret_cast<float4*>(C + o) = float4{out[0], out[1], out[2], out[3]};
     if (rmax) {
-      // max |row piece| over the wave's 256 columns, one atomic per row and wave
-#pragma unroll
-      for (int w = 1; w < 64; w <<= 1) mx = fmaxf(mx, __shfl_xor(mx, w));
-      if (threadIdx.x == 0) atomicMax(rmax + m, __float_as_uint(mx));
+      // max |row piece| over the wave's 256 columns by DPP (within each
+      // 16-lane row, then row_bcast:15 / row_bcast:31 into lane 63: VALU
+      // only, no LDS permutes), one atomic per row and wave
+#define ZF_DMAX(CTRL, ROWS) \
+  mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(mx), __float_as_int(mx), CTRL, ROWS, 0xF, false)))
+      ZF_DMAX(0xB1, 0xF);   // quad_perm [1, 0, 3, 2]
+      ZF_DMAX(0x4E, 0xF);   // quad_perm [2, 3, 0, 1]
+      ZF_DMAX(0x141, 0xF);  // row_half_mirror
+      ZF_DMAX(0x140, 0xF);  // row_mirror: every lane has its 16-lane row's max
+      ZF_DMAX(0x142, 0xA);  // row_bcast:15 into rows 1 and 3
+      ZF_DMAX(0x143, 0xC);  // row_bcast:31 into rows 2 and 3: lane 63 has the wave's max
+#undef ZF_DMAX
+      if (threadIdx.x == 63) atomicMax(rmax + m, __float_as_uint(mx));
     }
   }
 }
