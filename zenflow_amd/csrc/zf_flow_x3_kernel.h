@@ -393,6 +393,19 @@ __device__ __forceinline__ void load_frag(const char* a, typename XT<NT>::E (&f)
 // scales on the accumulator: us = 2^-(e_act + kw) (ius = 1/us).  Returned
 // in isc: the swish constant c = isc*log2(e) (act_swish).  Lanes l and l^32
 // hold the same sample.
+// The two wave halves' copies of x (lane l and lane l ^ 32 hold the same
+// sample): .lo = the value of lane l & 31, .hi = that of lane l | 32, on
+// every lane.  One v_permlane32_swap (VALU; gfx950) instead of the
+// ds_bpermute an __shfl_xor(x, 32) lowers to (an LDS round trip, in the
+// kernel's serial spline phase), and no select to pick the halves.
+struct X3Halves {
+  float lo, hi;
+};
+__device__ __forceinline__ X3Halves x3_halves(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+  return {__int_as_float(r[0]), __int_as_float(r[1])};
+}
+
 template <int T, bool OACT = false>
 __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, float& isc, float& us, float& ius,
                                              int act = ZF_ACT_SWISH) {
@@ -401,7 +414,10 @@ __device__ __forceinline__ void x3_act_scale(const floatx16 (&hb)[T], int kw, fl
   for (int t = 0; t < T; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(hb[t][r]));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  {
+    const X3Halves q = x3_halves(m);
+    m = fmaxf(q.lo, q.hi);
+  }
   // OACT: |act(v)| <= |v| for every activation the kernel takes (relu,
   // leaky_relu, tanh, gelu, elu, and sigmoid / softplus centred:
   // act_tile_centered), so the bound holds as for swish.
@@ -1597,7 +1613,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
       float eU = 0.f, eisc = 1.f, eus = 1.f, eius = 1.f;  // kEarly: bound and scales of the current layer input
       halfx8 ecs[2];  // kEarly: k-step-0 split of the current layer input's tile 0
       if constexpr (kEarly) {
-        umax = fmaxf(umax, __shfl_xor(umax, 32));
+        const X3Halves uq = x3_halves(umax);
+        umax = fmaxf(uq.lo, uq.hi);
         eU = __builtin_fmaf(op.x3_rb[0][0], umax, op.x3_rb[0][1]);
         x3_scale_from(eU, nh > 1 ? opc.kw1 : kw_last, eisc, eus, eius);
         x3_act_tile<NT, false>(hb[0], eisc, act);
@@ -1663,7 +1680,8 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
 #pragma unroll
           for (int o = 0; o < T; ++o) hb[o] = acc[o];
           eU = nU; eisc = nisc; eus = nus; eius = nius;
-          eM = fmaxf(mx, __shfl_xor(mx, 32));
+          const X3Halves mq = x3_halves(mx);
+          eM = fmaxf(mq.lo, mq.hi);
         }
       } else
       for (int l = 1; l < nh; ++l) {
@@ -1790,14 +1808,12 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
           for (int r = 0; r < 16; ++r) {
             if constexpr (kSplitWH) {
               if (o == 0) P[r] = pa[0][r];
-              else {  // slope r of half 0, on both halves
-                const float other = __shfl_xor(pa[1][r], 32);
-                P[2 * K + r] = hh == 0 ? pa[1][r] : other;
-              }
+              else  // slope r of half 0, on both halves
+                P[2 * K + r] = x3_halves(pa[1][r]).lo;
             } else if constexpr (ONE) {  // both halves end up with all of the dim's parameters
-              const float other = __shfl_xor(pa[o][r], 32);
-              P[32 * o + r] = hh == 0 ? pa[o][r] : other;
-              P[32 * o + 16 + r] = hh == 0 ? other : pa[o][r];
+              const X3Halves q = x3_halves(pa[o][r]);
+              P[32 * o + r] = q.lo;
+              P[32 * o + 16 + r] = q.hi;
             } else {
               P[16 * o + r] = pa[o][r];
             }
@@ -1842,10 +1858,9 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
               const float a = rcp_refined(sw) * kc.rnorm;
 #pragma unroll
               for (int j = 0; j < K; ++j) {
-                const float f = __builtin_fmaf(w[j], a, bc);
-                const float other = __shfl_xor(f, 32);
-                w[j] = hh == 0 ? f : other;
-                hg[j] = hh == 0 ? other : f;
+                const X3Halves q = x3_halves(__builtin_fmaf(w[j], a, bc));
+                w[j] = q.lo;
+                hg[j] = q.hi;
               }
             } else {
               float sx = 0.f, sy = 0.f;
@@ -1892,9 +1907,9 @@ __global__ __launch_bounds__(kX3Waves * 64, (x3_occupancy<T, K, PAIRS>())) void 
         }
         wave_lds_sync();
         if (!INV) {
-          const float other = __shfl_xor(ldv, 32);
-          ldn = ldn + (hh == 0 ? ldv : other);
-          if (2 * pr + 1 < dt) ldn = ldn + (hh == 0 ? other : ldv);
+          const X3Halves q = x3_halves(ldv);
+          ldn = ldn + q.lo;
+          if (2 * pr + 1 < dt) ldn = ldn + q.hi;
         }
       }
       if (!INV) ld = ld + ldn;  // Chain: log_det += ld (bijectors.py:110)
