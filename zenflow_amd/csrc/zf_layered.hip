@@ -152,6 +152,11 @@ constexpr int kX3RS = 40;              // halfs per LDS row (32 k + 8 pad = 80 B
 #define ZF_H2_DB 1
 #endif
 constexpr bool kH2DB = ZF_H2_DB != 0;
+// resident blocks per CU the kernel is built and launched for (tuning: 3
+// needs the single-buffer stage's LDS and spills a few VGPRs)
+#ifndef ZF_H2_OCC
+#define ZF_H2_OCC 2
+#endif
 constexpr int kH2RS = kH2DB ? 32 : kX3RS;  // halfs per LDS row
 constexpr int kH2Pl = 128 * kH2RS;         // halfs per plane
 constexpr int kH2Buf = 4 * kH2Pl;          // one stage: A hi, A lo, B hi, B lo
@@ -235,7 +240,7 @@ __device__ __forceinline__ float h2_act(int act, float v) {
 }
 
 template <bool WIDE, bool SW>
-__global__ __launch_bounds__(256, 2) void gemm_h2_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+__global__ __launch_bounds__(256, ZF_H2_OCC) void gemm_h2_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                       const _Float16* __restrict__ Wp, const unsigned* __restrict__ rin,
                                                       int kw, float* __restrict__ C, int ldc,
                                                       const float* __restrict__ bias, float* __restrict__ H,
@@ -444,7 +449,7 @@ int dense_gemm_h2(int M, int N, int K, const float* A, int lda, const void* Wp, 
   const long long ntiles = (long long)((N + kX3BN - 1) / kX3BN) * ((M + kX3BM - 1) / kX3BM);
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const dim3 grid((unsigned)std::min<long long>(ntiles, 2ll * ncu));
+  const dim3 grid((unsigned)std::min<long long>(ntiles, (long long)ZF_H2_OCC * ncu));
   const bool wide = N % 4 == 0 && ldc % 4 == 0 && (!C || al16(C)) && (!H || al16(H));
   const _Float16* W = static_cast<const _Float16*>(Wp);
   const bool sw = act == ZF_ACT_SWISH || !H;  // no activation stored: the swish-only form
